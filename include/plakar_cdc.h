@@ -1,0 +1,198 @@
+/*
+ * plakar_cdc.h — C ABI of the MI355X content-defined chunker (libplakar_cdc.so).
+ *
+ * Drop-in boundary for plakar's chunking path.  Every entry point below names
+ * the reference interface it replaces.  Reference paths are relative to the
+ * plakar tree; "ext" marks the third-party Go module
+ * github.com/PlakarKorp/go-cdc-chunkers v0.0.8 (go.mod:37), whose source is not
+ * vendored in the reference.
+ *
+ * Plain C types only: no HIP or torch types appear in any signature.  Device
+ * pointers are `void *`, and HIP streams are passed as `void *` (a hipStream_t,
+ * or NULL for the null stream).  No call throws.  Every call returns an int
+ * status: CDC_OK / CDC_EOF / CDC_NEED_DATA (>= 0) or a negative CDC_E_* code.
+ * cdc_strerror() turns a status into text.
+ *
+ * The product never falls back to the CPU.  If no GPU is present, or the HIP
+ * runtime fails, calls return CDC_E_DEVICE / CDC_E_NO_DEVICE.
+ */
+#ifndef PLAKAR_CDC_H
+#define PLAKAR_CDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CDC_ABI_VERSION 1
+
+/* ---- status codes --------------------------------------------------------- */
+#define CDC_OK 0
+#define CDC_EOF 1           /* io.EOF: the stream is drained (Next() returned its last chunk) */
+#define CDC_NEED_DATA 2     /* streaming: append more bytes (or mark EOF) before the next chunk */
+#define CDC_E_INVALID (-1)  /* bad argument (NULL pointer, bad length, misaligned, ...) */
+#define CDC_E_UNSUPPORTED (-2) /* algorithm not implemented here (e.g. "ultracdc") */
+#define CDC_E_NOSPACE (-3)  /* output array too small; the needed count is reported */
+#define CDC_E_DEVICE (-4)   /* HIP runtime / kernel failure */
+#define CDC_E_NOMEM (-5)    /* host or device allocation failed */
+#define CDC_E_NORMAL_SIZE (-6) /* ext fastcdc ErrNormalSize */
+#define CDC_E_MIN_SIZE (-7)    /* ext fastcdc ErrMinSize */
+#define CDC_E_MAX_SIZE (-8)    /* ext fastcdc ErrMaxSize */
+#define CDC_E_IO (-9)       /* a reader callback reported an error */
+#define CDC_E_NOT_INIT (-10) /* cdc_init() has not been called */
+#define CDC_E_NO_DEVICE (-11) /* no HIP device visible */
+
+/* ---- data types -------------------------------------------------------------- */
+
+/* chunkers.ChunkerOpts (ext chunker.go; used at repository/repository.go:288-292,
+ * chunking/chunking_test.go:19-23).  Sizes in bytes. */
+typedef struct cdc_opts {
+    uint32_t min_size;
+    uint32_t normal_size;
+    uint32_t max_size;
+    uint32_t reserved; /* must be 0 */
+} cdc_opts;
+
+/* One chunk: [offset, offset + length) of its buffer.  plakar stores only the
+ * length (objects.Chunk.Length, objects/objects.go:73-79); the offsets are the
+ * prefix sums the VFS walks (snapshot/vfs/vfilep.go:30-49). */
+typedef struct cdc_cut {
+    uint64_t offset;
+    uint32_t length;
+    uint32_t reserved;
+} cdc_cut;
+
+/* An independent input buffer (one file, or a window of one). */
+typedef struct cdc_buf {
+    const void *data;
+    uint64_t len;
+} cdc_buf;
+
+/* Device-side result block, written by the device path.  Read it after the
+ * stream has been synchronised. */
+typedef struct cdc_result {
+    uint64_t ncuts;    /* chunks written (final chunk included when final != 0) */
+    uint64_t consumed; /* bytes covered by the written chunks (== len when final) */
+    int64_t status;    /* CDC_OK, or CDC_E_NOSPACE */
+    uint64_t needed;   /* chunks needed when status == CDC_E_NOSPACE */
+} cdc_result;
+
+/* ---- library setup ------------------------------------------------------------ */
+
+/* Initialise the library on the devices in dev_mask (bit i = HIP device i;
+ * 0 = every visible device).  gear = 256-entry Gear table of
+ * ext chunkers/fastcdc (the package-level G), or NULL for the built-in
+ * placeholder table (see cdc_default_gear).  mask_s / mask_l = the FastCDC
+ * small/large masks (0 selects the defaults 0x0003590703530000 /
+ * 0x0000d90003530000).  cut_convention: 0 = Algorithm returns i (the chunk
+ * excludes the byte whose fingerprint matched), 1 = returns i + 1.
+ * May be called again to change the parameters; it is not reentrant with
+ * in-flight chunking calls. */
+int cdc_init(uint32_t dev_mask, const uint64_t gear[256], uint64_t mask_s, uint64_t mask_l,
+             int cut_convention);
+void cdc_shutdown(void);
+const char *cdc_strerror(int status);
+int cdc_abi_version(void);
+int cdc_device_count(void);
+
+/* The built-in Gear table: a PLACEHOLDER (splitmix64 from a fixed seed).  The
+ * v0.0.8 table of ext chunkers/fastcdc is not available in this build (see
+ * DESIGN.md, "Oracle").  Pass the real table to cdc_init() once it is. */
+void cdc_default_gear(uint64_t out[256]);
+uint64_t cdc_default_mask_s(void);
+uint64_t cdc_default_mask_l(void);
+
+/* ext fastcdc (*FastCDC).Validate + chunkers.NewChunker's registry lookup
+ * (algorithm names are matched after lower-casing, as
+ * repository/repository.go:288 does).  Returns CDC_OK, CDC_E_UNSUPPORTED or
+ * CDC_E_{NORMAL,MIN,MAX}_SIZE. */
+int cdc_validate(const char *algorithm, const cdc_opts *opts);
+
+/* chunking.DefaultConfiguration() (chunking/chunking.go:10-17). */
+void cdc_default_opts(cdc_opts *out);
+
+/* ---- batch path: host buffers in, host cut lists out ---------------------------
+ * Replaces the per-file loop `chk := repo.Chunker(rd); for { chk.Next() }`
+ * (snapshot/backup.go:647-665) for a batch of whole files already in host
+ * memory.  Each buffer is chunked independently, as one complete stream.
+ * out receives the cuts of buffer 0, then buffer 1, ...; out_counts[i] = the
+ * number of cuts of buffer i.  If out_cap is too small, returns CDC_E_NOSPACE
+ * with *out_needed set (out_needed may be NULL).  Synchronous. */
+int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out,
+              uint64_t out_cap, uint64_t *out_counts, uint64_t *out_needed);
+
+/* ---- device-resident path -----------------------------------------------------
+ * d_data: device pointer to len bytes (any alignment) on `device`.
+ * final != 0: the buffer is a whole stream, so the last chunk ends at len.
+ * final == 0: more bytes follow.  Only chunks whose cut is decided by the
+ * bytes present are written, and result->consumed tells the caller where to
+ * resume (the Peek(MaxSize) window of ext chunker.go).
+ * d_cuts / d_result: device memory.  d_workspace: device memory of at least
+ * cdc_device_workspace_size() bytes, not shared with another in-flight call.
+ * Asynchronous on `stream`: enqueues kernels and returns.  Graph-capturable. */
+int cdc_device_workspace_size(uint64_t len, const cdc_opts *opts, uint64_t *bytes);
+int cdc_chunk_device_async(int device, const void *d_data, uint64_t len, int final,
+                           const cdc_opts *opts, cdc_cut *d_cuts, uint64_t cut_cap,
+                           cdc_result *d_result, void *d_workspace, uint64_t workspace_bytes,
+                           void *stream);
+
+/* Batched device path: nbufs independent device buffers chunked by one set of
+ * launches.  d_cuts[i] / cut_caps[i] / d_results[i] are per buffer.  The
+ * workspace must be at least cdc_device_batch_workspace_size() bytes. */
+int cdc_device_batch_workspace_size(const uint64_t *lens, int nbufs, const cdc_opts *opts,
+                                    uint64_t *bytes);
+int cdc_chunk_device_batch_async(int device, const void *const *d_data, const uint64_t *lens,
+                                 int nbufs, int final, const cdc_opts *opts,
+                                 cdc_cut *const *d_cuts, const uint64_t *cut_caps,
+                                 cdc_result *const *d_results, void *d_workspace,
+                                 uint64_t workspace_bytes, void *stream);
+
+/* ---- streaming chunker: chunkers.NewChunker / (*Chunker).Next -----------------
+ * Push model, so cgo never hands a Go pointer to asynchronous HIP work: the
+ * caller appends stream bytes into a pinned staging window the library owns
+ * (cdc_stream_buffer + cdc_stream_commit), then drains chunks with
+ * cdc_stream_next.  A chunk pointer aliases that window and stays valid until
+ * the next call on the same stream, like the slice ext (*Chunker).Next returns
+ * (it aliases the bufio buffer).
+ *   cdc_stream_next -> CDC_OK        chunk and len receive the next chunk
+ *                   -> CDC_NEED_DATA append bytes (or commit with eof = 1)
+ *                   -> CDC_EOF       no more chunks (io.EOF)
+ * window_bytes = 0 picks a default (>= 2 * max_size). */
+typedef struct cdc_stream cdc_stream;
+int cdc_stream_new(const char *algorithm, const cdc_opts *opts, uint64_t window_bytes, int device,
+                   cdc_stream **out);
+int cdc_stream_buffer(cdc_stream *s, uint8_t **write_ptr, uint64_t *space);
+int cdc_stream_commit(cdc_stream *s, uint64_t nbytes, int eof);
+int cdc_stream_next(cdc_stream *s, const uint8_t **chunk, uint64_t *len);
+void cdc_stream_free(cdc_stream *s);
+
+/* Pull-model convenience over cdc_stream (an io.Reader as a callback):
+ * read(ctx, buf, cap) returns the number of bytes read, 0 at EOF, < 0 on error. */
+typedef int64_t (*cdc_read_fn)(void *ctx, void *buf, uint64_t cap);
+typedef struct cdc_chunker cdc_chunker;
+int cdc_chunker_new(const char *algorithm, cdc_read_fn read, void *ctx, const cdc_opts *opts,
+                    cdc_chunker **out);
+int cdc_chunker_next(cdc_chunker *c, const uint8_t **chunk, uint64_t *len);
+void cdc_chunker_free(cdc_chunker *c);
+
+/* ---- diagnostics ---------------------------------------------------------------
+ * Kernel selection for tests: 0 = default (scan + index + speculative
+ * resolution), 1 = force the sequential single-wave resolver (reference path
+ * on the device, for cross-checking the fast path). */
+int cdc_set_debug_mode(int mode);
+
+/* Live profiling of the device path: when enabled, every launch group records
+ * hipEvents on its stream before/after the scan kernel and after the last
+ * resolution kernel.  collect() waits for the recorded events, returns the
+ * summed scan time, summed pipeline time, number of launch groups and input
+ * bytes scanned since the last collect, and resets. */
+int cdc_profile_enable(int on);
+int cdc_profile_collect(double *scan_ms, double *pipeline_ms, uint64_t *launches,
+                        uint64_t *scan_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLAKAR_CDC_H */

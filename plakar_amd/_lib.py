@@ -1,0 +1,155 @@
+"""ctypes binding of libplakar_cdc.so (the C ABI declared in include/plakar_cdc.h).
+
+The product path always goes through this library: there is no CPU chunker in
+the package.  If the shared library is missing, import fails loudly with the
+command that builds it.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libplakar_cdc.so")
+
+CDC_OK = 0
+CDC_EOF = 1
+CDC_NEED_DATA = 2
+CDC_E_INVALID = -1
+CDC_E_UNSUPPORTED = -2
+CDC_E_NOSPACE = -3
+CDC_E_DEVICE = -4
+CDC_E_NOMEM = -5
+CDC_E_NORMAL_SIZE = -6
+CDC_E_MIN_SIZE = -7
+CDC_E_MAX_SIZE = -8
+CDC_E_IO = -9
+CDC_E_NOT_INIT = -10
+CDC_E_NO_DEVICE = -11
+
+
+class cdc_opts(ctypes.Structure):
+    _fields_ = [("min_size", ctypes.c_uint32), ("normal_size", ctypes.c_uint32),
+                ("max_size", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class cdc_cut(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class cdc_buf(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64)]
+
+
+class cdc_result(ctypes.Structure):
+    _fields_ = [("ncuts", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+                ("status", ctypes.c_int64), ("needed", ctypes.c_uint64)]
+
+
+CUT_DTYPE_FIELDS = [("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")]
+READ_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
+
+_P = ctypes.POINTER
+_u8p = _P(ctypes.c_uint8)
+
+# name -> (restype, argtypes); every symbol here is declared in include/plakar_cdc.h
+SIGNATURES = {
+    "cdc_abi_version": (ctypes.c_int, []),
+    "cdc_init": (ctypes.c_int, [ctypes.c_uint32, _P(ctypes.c_uint64), ctypes.c_uint64,
+                                ctypes.c_uint64, ctypes.c_int]),
+    "cdc_shutdown": (None, []),
+    "cdc_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "cdc_device_count": (ctypes.c_int, []),
+    "cdc_default_gear": (None, [_P(ctypes.c_uint64)]),
+    "cdc_default_mask_s": (ctypes.c_uint64, []),
+    "cdc_default_mask_l": (ctypes.c_uint64, []),
+    "cdc_validate": (ctypes.c_int, [ctypes.c_char_p, _P(cdc_opts)]),
+    "cdc_default_opts": (None, [_P(cdc_opts)]),
+    "cdc_chunk": (ctypes.c_int, [_P(cdc_buf), ctypes.c_int, _P(cdc_opts), _P(cdc_cut),
+                                 ctypes.c_uint64, _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
+    "cdc_device_workspace_size": (ctypes.c_int, [ctypes.c_uint64, _P(cdc_opts),
+                                                 _P(ctypes.c_uint64)]),
+    "cdc_chunk_device_async": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.c_int, _P(cdc_opts), ctypes.c_void_p,
+                                              ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_uint64, ctypes.c_void_p]),
+    "cdc_device_batch_workspace_size": (ctypes.c_int, [_P(ctypes.c_uint64), ctypes.c_int,
+                                                       _P(cdc_opts), _P(ctypes.c_uint64)]),
+    "cdc_chunk_device_batch_async": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_void_p),
+                                                    _P(ctypes.c_uint64), ctypes.c_int,
+                                                    ctypes.c_int, _P(cdc_opts),
+                                                    _P(ctypes.c_void_p), _P(ctypes.c_uint64),
+                                                    _P(ctypes.c_void_p), ctypes.c_void_p,
+                                                    ctypes.c_uint64, ctypes.c_void_p]),
+    "cdc_stream_new": (ctypes.c_int, [ctypes.c_char_p, _P(cdc_opts), ctypes.c_uint64,
+                                      ctypes.c_int, _P(ctypes.c_void_p)]),
+    "cdc_stream_buffer": (ctypes.c_int, [ctypes.c_void_p, _P(_u8p), _P(ctypes.c_uint64)]),
+    "cdc_stream_commit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]),
+    "cdc_stream_next": (ctypes.c_int, [ctypes.c_void_p, _P(_u8p), _P(ctypes.c_uint64)]),
+    "cdc_stream_free": (None, [ctypes.c_void_p]),
+    "cdc_chunker_new": (ctypes.c_int, [ctypes.c_char_p, READ_FN, ctypes.c_void_p, _P(cdc_opts),
+                                       _P(ctypes.c_void_p)]),
+    "cdc_chunker_next": (ctypes.c_int, [ctypes.c_void_p, _P(_u8p), _P(ctypes.c_uint64)]),
+    "cdc_chunker_free": (None, [ctypes.c_void_p]),
+    "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),
+                                           _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libplakar_cdc.so (once).  Raises if the HIP extension was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libplakar_cdc.so not found at {LIB_PATH}: the HIP extension is required "
+                "(build it with `python -m plakar_amd.build`); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class CdcError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        msg = lib().cdc_strerror(status).decode()
+        super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
+
+
+def check(status, what=""):
+    if status < 0:
+        raise CdcError(status, what)
+    return status
+
+
+_init_key = None
+
+
+def ensure_init(gear=None, mask_s=0, mask_l=0, cut_convention=0, dev_mask=0):
+    """cdc_init once per parameter set (the Gear table / masks are library-global,
+    like the package-level G of ext chunkers/fastcdc)."""
+    global _init_key
+    key = (None if gear is None else tuple(int(x) for x in gear), int(mask_s), int(mask_l),
+           int(cut_convention), int(dev_mask))
+    if key == _init_key:
+        return
+    arr = None
+    if gear is not None:
+        if len(gear) != 256:
+            raise ValueError("gear table must have 256 entries")
+        arr = (ctypes.c_uint64 * 256)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in gear])
+    check(lib().cdc_init(dev_mask, arr, mask_s, mask_l, cut_convention), "cdc_init")
+    _init_key = key
+
+
+def default_gear():
+    arr = (ctypes.c_uint64 * 256)()
+    lib().cdc_default_gear(arr)
+    return [int(x) for x in arr]

@@ -1,0 +1,56 @@
+"""Build libplakar_cdc.so (HIP, gfx950) in-tree and the CPU oracle (test infrastructure).
+
+    python -m plakar_amd.build            # both
+    python -m plakar_amd.build --lib-only
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the build
+container; the built .so travels to the GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_DIR = os.path.join(HERE, "_lib")
+LIB = os.path.join(LIB_DIR, "libplakar_cdc.so")
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("cdc_kernels.hip", "cdc_api.cpp")]
+HEADERS = [os.path.join(HERE, "csrc", "cdc_internal.h"), os.path.join(ROOT, "include", "plakar_cdc.h")]
+ARCH = os.environ.get("PLAKAR_CDC_ARCH", "gfx950")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force=False, verbose=True):
+    if not force and not _stale(LIB, SOURCES + HEADERS):
+        return LIB
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function",
+           "-o", tmp] + SOURCES
+    if verbose:
+        print("[plakar_amd.build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(verbose=True):
+    """Compile oracle/ (CPU checker; never linked into the product)."""
+    cmd = ["make", "-s", "-C", os.path.join(ROOT, "oracle")]
+    if verbose:
+        print("[plakar_amd.build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+
+
+if __name__ == "__main__":
+    build_lib(force="--force" in sys.argv)
+    if "--lib-only" not in sys.argv:
+        build_oracle()

@@ -1,0 +1,178 @@
+"""Mirror of the chunker API plakar consumes from ext go-cdc-chunkers v0.0.8.
+
+    chunkers.ChunkerOpts{MinSize, NormalSize, MaxSize}   (chunking/chunking_test.go:19-23)
+    chunkers.NewChunker(name, rd, opts)                  (repository/repository.go:288-292)
+    (*Chunker).Next() ([]byte, error)                    (snapshot/backup.go:651-665)
+
+Names, argument meaning and error behaviour follow the Go API: Next() returns
+(chunk, err) where err is None or EOF; the empty stream yields (None, EOF) at
+once.  Every chunk is cut on the GPU by libplakar_cdc.so (there is no CPU
+path): the stream is staged through a pinned window the library owns and
+chunked by the device kernels; ChunkBuffers is the batch form used by the
+re-plumbed backup (one call for many files).
+"""
+import ctypes
+
+from . import _lib
+from ._lib import CDC_EOF, CDC_NEED_DATA, CDC_OK, CdcError, check, ensure_init, lib
+
+
+class _EOFType(Exception):
+    """io.EOF."""
+
+    def __repr__(self):
+        return "EOF"
+
+
+EOF = _EOFType("EOF")
+
+
+class ChunkerOpts:
+    """chunkers.ChunkerOpts."""
+
+    __slots__ = ("MinSize", "NormalSize", "MaxSize")
+
+    def __init__(self, MinSize=0, NormalSize=0, MaxSize=0):
+        self.MinSize = int(MinSize)
+        self.NormalSize = int(NormalSize)
+        self.MaxSize = int(MaxSize)
+
+    def __eq__(self, other):
+        return (isinstance(other, ChunkerOpts) and self.MinSize == other.MinSize
+                and self.NormalSize == other.NormalSize and self.MaxSize == other.MaxSize)
+
+    def __repr__(self):
+        return (f"ChunkerOpts(MinSize={self.MinSize}, NormalSize={self.NormalSize}, "
+                f"MaxSize={self.MaxSize})")
+
+    def _c(self):
+        return _lib.cdc_opts(self.MinSize, self.NormalSize, self.MaxSize, 0)
+
+
+def FastCDCDefaultOptions():
+    """(*FastCDC).DefaultOptions(): used when NewChunker gets nil options."""
+    return ChunkerOpts(MinSize=2 * 1024, NormalSize=8 * 1024, MaxSize=64 * 1024)
+
+
+def Validate(algorithm, opts):
+    """chunkers.NewChunker's registry lookup + (*FastCDC).Validate; raises CdcError."""
+    o = opts._c()
+    check(lib().cdc_validate(algorithm.encode(), ctypes.byref(o)), "NewChunker")
+
+
+class Chunker:
+    """*chunkers.Chunker over an io.Reader-like object (read(n) / readinto)."""
+
+    def __init__(self, algorithm, reader, opts, window_bytes=0, device=0):
+        ensure_init()
+        self._rd = reader
+        self._opts = opts
+        self._h = ctypes.c_void_p()
+        o = opts._c()
+        check(lib().cdc_stream_new(algorithm.encode(), ctypes.byref(o), window_bytes, device,
+                                   ctypes.byref(self._h)), "NewChunker")
+        self._eof = False
+
+    def _fill(self):
+        L = lib()
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        space = ctypes.c_uint64()
+        check(L.cdc_stream_buffer(self._h, ctypes.byref(ptr), ctypes.byref(space)))
+        n = space.value
+        if n == 0:
+            return
+        dst = (ctypes.c_uint8 * n).from_address(ctypes.addressof(ptr.contents))
+        view = memoryview(dst).cast("B")
+        got = 0
+        readinto = getattr(self._rd, "readinto", None)
+        while got < n:
+            if readinto is not None:
+                k = readinto(view[got:])
+            else:
+                data = self._rd.read(n - got)
+                k = len(data)
+                view[got:got + k] = data
+            if not k:
+                self._eof = True
+                break
+            got += k
+        check(L.cdc_stream_commit(self._h, got, 1 if self._eof else 0))
+
+    def Next(self):
+        """Return (chunk bytes, None), or (None, EOF) once the stream is drained."""
+        L = lib()
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        ln = ctypes.c_uint64()
+        while True:
+            st = L.cdc_stream_next(self._h, ctypes.byref(ptr), ctypes.byref(ln))
+            if st == CDC_OK:
+                return ctypes.string_at(ptr, ln.value), None
+            if st == CDC_EOF:
+                return None, EOF
+            if st == CDC_NEED_DATA:
+                self._fill()
+                continue
+            raise CdcError(st, "Next")
+
+    def __iter__(self):
+        while True:
+            chunk, err = self.Next()
+            if err is EOF:
+                return
+            yield chunk
+
+    def close(self):
+        if self._h:
+            lib().cdc_stream_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def NewChunker(algorithm, reader, opts=None, window_bytes=0):
+    """chunkers.NewChunker(algorithm, rd, opts); raises CdcError for an unknown
+    algorithm or invalid sizes (the Go call returns them as its error)."""
+    if opts is None:
+        opts = FastCDCDefaultOptions()
+    Validate(algorithm, opts)
+    return Chunker(algorithm, reader, opts, window_bytes=window_bytes)
+
+
+def ChunkBuffers(bufs, opts):
+    """Batch API of the re-plumbed backup: chunk whole in-memory files on the
+    GPU(s) in one call.  Returns, per buffer, a uint64 array of shape (n, 2)
+    holding (offset, length) rows."""
+    import numpy as np
+
+    ensure_init()
+    o = opts._c()
+    check(lib().cdc_validate(b"fastcdc", ctypes.byref(o)), "ChunkBuffers")
+    n = len(bufs)
+    keep = []
+    cbufs = (_lib.cdc_buf * max(n, 1))()
+    total_cap = 0
+    for i, b in enumerate(bufs):
+        a = np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        keep.append(a)
+        cbufs[i].data = a.ctypes.data if a.size else None
+        cbufs[i].len = a.size
+        total_cap += a.size // max(opts.MinSize, 1) + 2
+    out = np.zeros((max(total_cap, 1), 2), dtype=np.uint64)
+    counts = (ctypes.c_uint64 * max(n, 1))()
+    needed = ctypes.c_uint64()
+    check(lib().cdc_chunk(cbufs, n, ctypes.byref(o),
+                          ctypes.cast(out.ctypes.data, ctypes.POINTER(_lib.cdc_cut)),
+                          out.shape[0], counts, ctypes.byref(needed)), "ChunkBuffers")
+    res, k = [], 0
+    for i in range(n):
+        c = counts[i]
+        part = out[k:k + c].copy()
+        part[:, 1] &= np.uint64(0xFFFFFFFF)
+        res.append(part)
+        k += c
+    return res

@@ -1,0 +1,818 @@
+// C-ABI implementation of libplakar_cdc.so (see include/plakar_cdc.h).
+//
+// Host runtime around the HIP kernels: per-device contexts (Gear table in
+// device memory, a stream, pinned staging + device arenas for the host-buffer
+// path), the batch / device-resident entry points, and the streaming chunker
+// that mirrors ext go-cdc-chunkers (*Chunker).Next.  No CPU chunking fallback
+// exists: without a device every compute entry point fails with a status.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cdc_internal.h"
+
+using namespace cdc;
+
+namespace {
+
+constexpr uint64_t kDefaultMaskS = 0x0003590703530000ull;  // FastCDC paper MaskS (15 bits)
+constexpr uint64_t kDefaultMaskL = 0x0000d90003530000ull;  // FastCDC paper MaskL (11 bits)
+
+struct DeviceCtx {
+    int device = -1;
+    uint64_t *d_gear = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // host-buffer path arenas (grown on demand)
+    uint8_t *h_stage = nullptr;
+    uint8_t *d_in = nullptr;
+    uint64_t in_cap = 0;
+    void *d_ws = nullptr;
+    uint64_t ws_cap = 0;
+    cdc_cut *d_cuts = nullptr;
+    cdc_cut *h_cuts = nullptr;
+    uint64_t cuts_cap = 0;
+    cdc_result *d_res = nullptr;
+    cdc_result *h_res = nullptr;
+};
+
+struct Global {
+    std::mutex mu;
+    bool init = false;
+    uint64_t gear[256];
+    uint64_t mask_s = kDefaultMaskS, mask_l = kDefaultMaskL;
+    uint32_t cut_adj = 0;
+    int debug_mode = 0;
+    std::vector<DeviceCtx *> devs;
+};
+
+Global &G()
+{
+    static Global g;
+    return g;
+}
+
+uint64_t splitmix64(uint64_t &s)
+{
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+std::string lower(const char *s)
+{
+    std::string r = s ? s : "";
+    for (auto &c : r) c = char(std::tolower((unsigned char)c));
+    return r;
+}
+
+int validate_sizes(const cdc_opts *o)
+{
+    // ext chunkers/fastcdc (*FastCDC).Validate: 64 B <= sizes <= 1 GiB, Min < Normal < Max
+    const uint64_t lo = 64, hi = 1ull << 30;
+    if (o->normal_size < lo || o->normal_size > hi) return CDC_E_NORMAL_SIZE;
+    if (o->min_size < lo || o->min_size > hi || o->min_size >= o->normal_size) return CDC_E_MIN_SIZE;
+    if (o->max_size < lo || o->max_size > hi || o->max_size <= o->normal_size) return CDC_E_MAX_SIZE;
+    return CDC_OK;
+}
+
+DevParams make_params(const cdc_opts *o)
+{
+    Global &g = G();
+    DevParams P;
+    P.min_size = o->min_size;
+    P.normal_size = o->normal_size;
+    P.max_size = o->max_size;
+    P.ms_lo = uint32_t(g.mask_s);
+    P.ms_hi = uint32_t(g.mask_s >> 32);
+    P.ml_lo = uint32_t(g.mask_l);
+    P.ml_hi = uint32_t(g.mask_l >> 32);
+    P.cut_adj = g.cut_adj;
+    const uint64_t m = g.mask_s | g.mask_l;
+    P.win = 64u - uint32_t(__builtin_clzll(m));
+    return P;
+}
+
+#define HIPCHK(x)                            \
+    do {                                     \
+        if ((x) != hipSuccess) return CDC_E_DEVICE; \
+    } while (0)
+
+void free_ctx_buffers(DeviceCtx *c)
+{
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->d_in) (void)hipFree(c->d_in);
+    if (c->d_ws) (void)hipFree(c->d_ws);
+    if (c->d_cuts) (void)hipFree(c->d_cuts);
+    if (c->h_cuts) (void)hipHostFree(c->h_cuts);
+    if (c->d_res) (void)hipFree(c->d_res);
+    if (c->h_res) (void)hipHostFree(c->h_res);
+    c->h_stage = c->d_in = nullptr;
+    c->d_ws = nullptr;
+    c->d_cuts = c->h_cuts = nullptr;
+    c->d_res = c->h_res = nullptr;
+    c->in_cap = c->ws_cap = c->cuts_cap = 0;
+}
+
+int grow(DeviceCtx *c, uint64_t in_bytes, uint64_t ws_bytes, uint64_t ncuts)
+{
+    if (in_bytes > c->in_cap) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        if (c->d_in) (void)hipFree(c->d_in);
+        c->h_stage = nullptr;
+        c->d_in = nullptr;
+        c->in_cap = 0;
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), in_bytes, hipHostMallocDefault));
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&c->d_in), in_bytes));
+        c->in_cap = in_bytes;
+    }
+    if (ws_bytes > c->ws_cap) {
+        if (c->d_ws) (void)hipFree(c->d_ws);
+        c->d_ws = nullptr;
+        c->ws_cap = 0;
+        HIPCHK(hipMalloc(&c->d_ws, ws_bytes));
+        c->ws_cap = ws_bytes;
+    }
+    if (ncuts > c->cuts_cap) {
+        if (c->d_cuts) (void)hipFree(c->d_cuts);
+        if (c->h_cuts) (void)hipHostFree(c->h_cuts);
+        c->d_cuts = c->h_cuts = nullptr;
+        c->cuts_cap = 0;
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&c->d_cuts), ncuts * sizeof(cdc_cut)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_cuts), ncuts * sizeof(cdc_cut),
+                             hipHostMallocDefault));
+        c->cuts_cap = ncuts;
+    }
+    if (!c->d_res) {
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&c->d_res), kMaxBufsPerLaunch * sizeof(cdc_result)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_res),
+                             kMaxBufsPerLaunch * sizeof(cdc_result), hipHostMallocDefault));
+    }
+    return CDC_OK;
+}
+
+Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
+{
+    char *b = static_cast<char *>(ws);
+    Workspace W;
+    W.blk_cnt = reinterpret_cast<uint32_t *>(b + pl.off_blk_cnt);
+    W.blk_ent = reinterpret_cast<uint16_t *>(b + pl.off_blk_ent);
+    W.w1_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w1_nodes);
+    W.w1_cnt = reinterpret_cast<uint32_t *>(b + pl.off_w1_cnt);
+    W.w2_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w2_nodes);
+    W.w2_cnt = reinterpret_cast<uint32_t *>(b + pl.off_w2_cnt);
+    W.w2_conv = reinterpret_cast<uint32_t *>(b + pl.off_w2_conv);
+    W.w2_idx = reinterpret_cast<uint32_t *>(b + pl.off_w2_idx);
+    W.w2_term = reinterpret_cast<uint64_t *>(b + pl.off_w2_term);
+    W.flags = reinterpret_cast<uint32_t *>(b + pl.off_flags);
+    W.gear = gear;
+    return W;
+}
+
+// Launch one group of <= kMaxBufsPerLaunch device buffers.
+int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const uint64_t *lens,
+              int n, int final_, cdc_cut *const *cuts, const uint64_t *caps,
+              cdc_result *const *res, void *ws, uint64_t ws_bytes, void *stream)
+{
+    Plan pl;
+    int st = make_plan(lens, n, P, &pl);
+    if (st != CDC_OK) return st;
+    if (ws_bytes < pl.bytes) return CDC_E_INVALID;
+    Batch B;
+    std::memset(&B, 0, sizeof(B));
+    B.nbufs = uint32_t(n);
+    B.final_ = final_ ? 1u : 0u;
+    B.total_segs = pl.total_segs;
+    B.total_blks = pl.total_blks;
+    B.total_tasks = pl.total_tasks;
+    B.cap1 = pl.cap1;
+    B.cap2 = pl.cap2;
+    B.seg = pl.seg;
+    B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
+    uint32_t segs = 0, blks = 0, tasks = 0;
+    for (int i = 0; i < n; ++i) {
+        BufDesc &D = B.b[i];
+        D.data = static_cast<const uint8_t *>(data[i]);
+        D.len = lens[i];
+        D.out = cuts[i];
+        D.cap = caps[i];
+        D.res = res[i];
+        D.seg_base = segs;
+        D.nseg = uint32_t((lens[i] + pl.seg - 1) / pl.seg);
+        D.blk_base = blks;
+        D.task_base = tasks;
+        segs += D.nseg;
+        blks += uint32_t((lens[i] + kIdxBlock - 1) / kIdxBlock);
+        tasks += uint32_t((lens[i] + kScanTaskBytes - 1) / kScanTaskBytes);
+    }
+    const Workspace W = carve(ws, pl, ctx->d_gear);
+    return launch_batch(B, P, W, stream);
+}
+
+int group_ws_bytes(const uint64_t *lens, int n, const DevParams &P, uint64_t *bytes)
+{
+    Plan pl;
+    const int st = make_plan(lens, n, P, &pl);
+    if (st != CDC_OK) return st;
+    *bytes = pl.bytes;
+    return CDC_OK;
+}
+
+int check_ready(int device, DeviceCtx **out)
+{
+    Global &g = G();
+    if (!g.init) return CDC_E_NOT_INIT;
+    for (auto *c : g.devs)
+        if (c->device == device) {
+            *out = c;
+            return CDC_OK;
+        }
+    return CDC_E_INVALID;
+}
+
+// Chunk one host buffer window-by-window on one device (used by cdc_chunk and
+// the streaming path).  Appends cuts (offsets relative to `base_off`).
+struct HostJob {
+    const uint8_t *data;
+    uint64_t len;
+    std::vector<cdc_cut> cuts;
+    int status = CDC_OK;
+};
+
+uint64_t max_cuts_for(uint64_t len, uint32_t min_size) { return len / min_size + 2; }
+
+// Process host jobs on one device: pack whole buffers into the arena; buffers
+// larger than the arena are chunked as streams of arena-sized windows.
+int run_host_jobs(DeviceCtx *ctx, const cdc_opts *o, std::vector<HostJob *> &jobs)
+{
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return CDC_E_DEVICE;
+    const DevParams P = make_params(o);
+    uint64_t arena = 256ull << 20;
+    if (const char *env = getenv("CDC_HOST_ARENA_MB")) {
+        const long v = atol(env);
+        if (v >= 16) arena = uint64_t(v) << 20;
+    }
+    arena = std::max<uint64_t>(arena, 4ull * o->max_size + 4096);
+    const uint64_t ncap = arena / o->min_size + 2 * kMaxBufsPerLaunch + 2;
+    int st = grow(ctx, arena, 0, ncap);
+    if (st != CDC_OK) return st;
+    // the workspace is sized per launch group, right before the launch
+    auto ensure_ws = [&](const uint64_t *lens, int n) {
+        uint64_t need = 0;
+        const int r = group_ws_bytes(lens, n, P, &need);
+        return r != CDC_OK ? r : grow(ctx, arena, need, ncap);
+    };
+
+    size_t j = 0;
+    while (j < jobs.size()) {
+        HostJob *job = jobs[j];
+        if (job->len > arena) {
+            // stream a large buffer through the arena
+            uint64_t off = 0;
+            while (off < job->len) {
+                const uint64_t w = std::min(arena, job->len - off);
+                const int fin = off + w == job->len;
+                std::memcpy(ctx->h_stage, job->data + off, w);
+                HIPCHK(hipMemcpyAsync(ctx->d_in, ctx->h_stage, w, hipMemcpyHostToDevice, ctx->stream));
+                const void *dp = ctx->d_in;
+                cdc_cut *cp = ctx->d_cuts;
+                const uint64_t cap = ctx->cuts_cap;
+                cdc_result *rp = ctx->d_res;
+                st = ensure_ws(&w, 1);
+                if (st != CDC_OK) return st;
+                st = run_group(ctx, P, &dp, &w, 1, fin, &cp, &cap, &rp, ctx->d_ws, ctx->ws_cap,
+                               ctx->stream);
+                if (st != CDC_OK) return st;
+                HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(cdc_result),
+                                      hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(hipStreamSynchronize(ctx->stream));
+                const cdc_result r = ctx->h_res[0];
+                if (r.status != CDC_OK) return int(r.status);
+                if (r.ncuts)
+                    HIPCHK(hipMemcpy(ctx->h_cuts, ctx->d_cuts, r.ncuts * sizeof(cdc_cut),
+                                     hipMemcpyDeviceToHost));
+                for (uint64_t k = 0; k < r.ncuts; ++k) {
+                    cdc_cut c = ctx->h_cuts[k];
+                    c.offset += off;
+                    job->cuts.push_back(c);
+                }
+                if (!fin && r.consumed == 0) return CDC_E_DEVICE;  // no progress: cannot happen
+                off += fin ? w : r.consumed;
+            }
+            ++j;
+            continue;
+        }
+        // pack as many whole buffers as fit
+        std::vector<HostJob *> group;
+        std::vector<uint64_t> offs, lens;
+        uint64_t used = 0;
+        while (j < jobs.size() && group.size() < size_t(kMaxBufsPerLaunch) &&
+               jobs[j]->len <= arena && used + jobs[j]->len <= arena) {
+            group.push_back(jobs[j]);
+            offs.push_back(used);
+            lens.push_back(jobs[j]->len);
+            used = (used + jobs[j]->len + 255) & ~255ull;
+            ++j;
+        }
+        for (size_t i = 0; i < group.size(); ++i)
+            std::memcpy(ctx->h_stage + offs[i], group[i]->data, group[i]->len);
+        if (used) HIPCHK(hipMemcpyAsync(ctx->d_in, ctx->h_stage, std::min(used, arena),
+                                        hipMemcpyHostToDevice, ctx->stream));
+        const int n = int(group.size());
+        std::vector<const void *> dp(n);
+        std::vector<cdc_cut *> cp(n);
+        std::vector<uint64_t> caps(n);
+        std::vector<cdc_result *> rp(n);
+        uint64_t cut_off = 0;
+        for (int i = 0; i < n; ++i) {
+            dp[i] = ctx->d_in + offs[i];
+            cp[i] = ctx->d_cuts + cut_off;
+            caps[i] = max_cuts_for(lens[i], o->min_size);
+            cut_off += caps[i];
+            rp[i] = ctx->d_res + i;
+        }
+        st = ensure_ws(lens.data(), n);
+        if (st != CDC_OK) return st;
+        st = run_group(ctx, P, dp.data(), lens.data(), n, 1, cp.data(), caps.data(), rp.data(),
+                       ctx->d_ws, ctx->ws_cap, ctx->stream);
+        if (st != CDC_OK) return st;
+        HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, n * sizeof(cdc_result),
+                              hipMemcpyDeviceToHost, ctx->stream));
+        if (cut_off)
+            HIPCHK(hipMemcpyAsync(ctx->h_cuts, ctx->d_cuts, cut_off * sizeof(cdc_cut),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        cut_off = 0;
+        for (int i = 0; i < n; ++i) {
+            const cdc_result r = ctx->h_res[i];
+            if (r.status != CDC_OK) return int(r.status);
+            group[i]->cuts.assign(ctx->h_cuts + cut_off, ctx->h_cuts + cut_off + r.ncuts);
+            cut_off += caps[i];
+        }
+    }
+    return CDC_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int cdc_abi_version(void) { return CDC_ABI_VERSION; }
+
+const char *cdc_strerror(int s)
+{
+    switch (s) {
+    case CDC_OK: return "ok";
+    case CDC_EOF: return "EOF";
+    case CDC_NEED_DATA: return "need more data";
+    case CDC_E_INVALID: return "invalid argument";
+    case CDC_E_UNSUPPORTED: return "unsupported chunking algorithm";
+    case CDC_E_NOSPACE: return "output capacity too small";
+    case CDC_E_DEVICE: return "HIP device error";
+    case CDC_E_NOMEM: return "out of memory";
+    case CDC_E_NORMAL_SIZE: return "NormalSize is required and must be 64B <= NormalSize <= 1GB";
+    case CDC_E_MIN_SIZE: return "MinSize is required and must be 64B <= MinSize <= 1GB && MinSize < NormalSize";
+    case CDC_E_MAX_SIZE: return "MaxSize is required and must be 64B <= MaxSize <= 1GB && MaxSize > NormalSize";
+    case CDC_E_IO: return "reader error";
+    case CDC_E_NOT_INIT: return "cdc_init() has not been called";
+    case CDC_E_NO_DEVICE: return "no HIP device available";
+    default: return "unknown status";
+    }
+}
+
+void cdc_default_gear(uint64_t out[256])
+{
+    uint64_t s = 0x504C414B4152ull;  // "PLAKAR"
+    for (int i = 0; i < 256; ++i) out[i] = splitmix64(s);
+}
+
+uint64_t cdc_default_mask_s(void) { return kDefaultMaskS; }
+uint64_t cdc_default_mask_l(void) { return kDefaultMaskL; }
+
+void cdc_default_opts(cdc_opts *out)
+{
+    if (!out) return;
+    out->min_size = 64 * 1024;
+    out->normal_size = 1 * 1024 * 1024;
+    out->max_size = 4 * 1024 * 1024;
+    out->reserved = 0;
+}
+
+int cdc_validate(const char *algorithm, const cdc_opts *opts)
+{
+    if (!algorithm || !opts) return CDC_E_INVALID;
+    const std::string a = lower(algorithm);
+    if (a != "fastcdc") return CDC_E_UNSUPPORTED;
+    return validate_sizes(opts);
+}
+
+int cdc_set_debug_mode(int mode)
+{
+    G().debug_mode = mode;
+    return CDC_OK;
+}
+
+int cdc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int cdc_init(uint32_t dev_mask, const uint64_t gear[256], uint64_t mask_s, uint64_t mask_l,
+             int cut_convention)
+{
+    Global &g = G();
+    std::lock_guard<std::mutex> lock(g.mu);
+    if (cut_convention != 0 && cut_convention != 1) return CDC_E_INVALID;
+    if (gear)
+        std::memcpy(g.gear, gear, sizeof(g.gear));
+    else
+        cdc_default_gear(g.gear);
+    g.mask_s = mask_s ? mask_s : kDefaultMaskS;
+    g.mask_l = mask_l ? mask_l : kDefaultMaskL;
+    g.cut_adj = uint32_t(cut_convention);
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        g.init = false;
+        return CDC_E_NO_DEVICE;
+    }
+    if (g.devs.empty()) {
+        for (int d = 0; d < n && d < 32; ++d) {
+            if (dev_mask && !(dev_mask & (1u << d))) continue;
+            auto *c = new DeviceCtx();
+            c->device = d;
+            if (hipSetDevice(d) != hipSuccess) return CDC_E_DEVICE;
+            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+                return CDC_E_DEVICE;
+            if (hipMalloc(reinterpret_cast<void **>(&c->d_gear), 256 * sizeof(uint64_t)) != hipSuccess)
+                return CDC_E_DEVICE;
+            g.devs.push_back(c);
+        }
+        if (g.devs.empty()) return CDC_E_NO_DEVICE;
+    }
+    for (auto *c : g.devs) {
+        if (hipSetDevice(c->device) != hipSuccess) return CDC_E_DEVICE;
+        if (hipMemcpy(c->d_gear, g.gear, sizeof(g.gear), hipMemcpyHostToDevice) != hipSuccess)
+            return CDC_E_DEVICE;
+    }
+    g.init = true;
+    return CDC_OK;
+}
+
+void cdc_shutdown(void)
+{
+    Global &g = G();
+    std::lock_guard<std::mutex> lock(g.mu);
+    for (auto *c : g.devs) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        free_ctx_buffers(c);
+        if (c->d_gear) (void)hipFree(c->d_gear);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        delete c;
+    }
+    g.devs.clear();
+    g.init = false;
+}
+
+int cdc_device_workspace_size(uint64_t len, const cdc_opts *opts, uint64_t *bytes)
+{
+    return cdc_device_batch_workspace_size(&len, 1, opts, bytes);
+}
+
+int cdc_device_batch_workspace_size(const uint64_t *lens, int nbufs, const cdc_opts *opts,
+                                    uint64_t *bytes)
+{
+    if (!lens || nbufs < 0 || !opts || !bytes) return CDC_E_INVALID;
+    const int v = validate_sizes(opts);
+    if (v != CDC_OK) return v;
+    const DevParams P = make_params(opts);
+    uint64_t best = 0;
+    for (int i = 0; i < nbufs; i += kMaxBufsPerLaunch) {
+        const int n = std::min(kMaxBufsPerLaunch, nbufs - i);
+        uint64_t b = 0;
+        const int st = group_ws_bytes(lens + i, n, P, &b);
+        if (st != CDC_OK) return st;
+        best = std::max(best, b);
+    }
+    *bytes = best;
+    return CDC_OK;
+}
+
+int cdc_chunk_device_async(int device, const void *d_data, uint64_t len, int final_,
+                           const cdc_opts *opts, cdc_cut *d_cuts, uint64_t cut_cap,
+                           cdc_result *d_result, void *d_workspace, uint64_t workspace_bytes,
+                           void *stream)
+{
+    return cdc_chunk_device_batch_async(device, &d_data, &len, 1, final_, opts, &d_cuts, &cut_cap,
+                                        &d_result, d_workspace, workspace_bytes, stream);
+}
+
+int cdc_chunk_device_batch_async(int device, const void *const *d_data, const uint64_t *lens,
+                                 int nbufs, int final_, const cdc_opts *opts,
+                                 cdc_cut *const *d_cuts, const uint64_t *cut_caps,
+                                 cdc_result *const *d_results, void *d_workspace,
+                                 uint64_t workspace_bytes, void *stream)
+{
+    if (!d_data || !lens || nbufs < 0 || !opts || !d_cuts || !cut_caps || !d_results ||
+        !d_workspace)
+        return CDC_E_INVALID;
+    const int v = validate_sizes(opts);
+    if (v != CDC_OK) return v;
+    DeviceCtx *ctx = nullptr;
+    int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    for (int i = 0; i < nbufs; ++i)
+        if (!d_results[i] || (lens[i] && (!d_data[i] || !d_cuts[i]))) return CDC_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    const DevParams P = make_params(opts);
+    for (int i = 0; i < nbufs; i += kMaxBufsPerLaunch) {
+        const int n = std::min(kMaxBufsPerLaunch, nbufs - i);
+        st = run_group(ctx, P, d_data + i, lens + i, n, final_, d_cuts + i, cut_caps + i,
+                       d_results + i, d_workspace, workspace_bytes, stream);
+        if (st != CDC_OK) return st;
+    }
+    return CDC_OK;
+}
+
+int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out, uint64_t out_cap,
+              uint64_t *out_counts, uint64_t *out_needed)
+{
+    if (nbufs < 0 || (nbufs > 0 && (!bufs || !out_counts)) || !opts) return CDC_E_INVALID;
+    const int v = validate_sizes(opts);
+    if (v != CDC_OK) return v;
+    Global &g = G();
+    if (!g.init) return CDC_E_NOT_INIT;
+    for (int i = 0; i < nbufs; ++i)
+        if (bufs[i].len && !bufs[i].data) return CDC_E_INVALID;
+    std::vector<HostJob> jobs(nbufs);
+    for (int i = 0; i < nbufs; ++i) {
+        jobs[i].data = static_cast<const uint8_t *>(bufs[i].data);
+        jobs[i].len = bufs[i].len;
+    }
+    // LPT assignment of buffers to devices (largest first onto the least loaded)
+    const size_t nd = g.devs.size();
+    std::vector<std::vector<HostJob *>> per(nd);
+    std::vector<uint64_t> load(nd, 0);
+    std::vector<int> order(nbufs);
+    for (int i = 0; i < nbufs; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return jobs[a].len > jobs[b].len; });
+    for (int i : order) {
+        if (jobs[i].len == 0) continue;
+        const size_t d = size_t(std::min_element(load.begin(), load.end()) - load.begin());
+        per[d].push_back(&jobs[i]);
+        load[d] += jobs[i].len;
+    }
+    std::vector<int> status(nd, CDC_OK);
+    std::vector<std::thread> threads;
+    for (size_t d = 0; d < nd; ++d) {
+        if (per[d].empty()) continue;
+        threads.emplace_back([&, d] {
+            // keep each device's buffers in input order inside its packing
+            std::sort(per[d].begin(), per[d].end());
+            status[d] = run_host_jobs(g.devs[d], opts, per[d]);
+        });
+    }
+    for (auto &t : threads) t.join();
+    for (int s : status)
+        if (s != CDC_OK) return s;
+    uint64_t total = 0;
+    for (auto &j : jobs) total += j.cuts.size();
+    if (out_needed) *out_needed = total;
+    if (total > out_cap || (total && !out)) {
+        for (int i = 0; i < nbufs; ++i) out_counts[i] = jobs[i].cuts.size();
+        return CDC_E_NOSPACE;
+    }
+    uint64_t k = 0;
+    for (int i = 0; i < nbufs; ++i) {
+        out_counts[i] = jobs[i].cuts.size();
+        if (!jobs[i].cuts.empty()) std::memcpy(out + k, jobs[i].cuts.data(), jobs[i].cuts.size() * sizeof(cdc_cut));
+        k += jobs[i].cuts.size();
+    }
+    return CDC_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Streaming chunker: ext go-cdc-chunkers (*Chunker).Next over a pinned window.
+// ===========================================================================
+struct cdc_stream {
+    int device = 0;
+    cdc_opts opts{};
+    DevParams P{};
+    uint64_t win = 0;
+    uint8_t *h_win = nullptr;  // pinned window; chunks alias it
+    uint8_t *d_win = nullptr;
+    void *d_ws = nullptr;
+    uint64_t ws_bytes = 0;
+    cdc_cut *d_cuts = nullptr, *h_cuts = nullptr;
+    uint64_t cuts_cap = 0;
+    cdc_result *d_res = nullptr, *h_res = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t fill = 0;      // bytes in the window
+    uint64_t consumed = 0;  // bytes covered by decided chunks of the last run
+    uint64_t ncuts = 0, next_cut = 0;
+    bool eof = false;
+    bool ran = false;
+};
+
+static void stream_release(cdc_stream *s)
+{
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->h_win) (void)hipHostFree(s->h_win);
+    if (s->d_win) (void)hipFree(s->d_win);
+    if (s->d_ws) (void)hipFree(s->d_ws);
+    if (s->d_cuts) (void)hipFree(s->d_cuts);
+    if (s->h_cuts) (void)hipHostFree(s->h_cuts);
+    if (s->d_res) (void)hipFree(s->d_res);
+    if (s->h_res) (void)hipHostFree(s->h_res);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+extern "C" int cdc_stream_new(const char *algorithm, const cdc_opts *opts, uint64_t window_bytes,
+                              int device, cdc_stream **out)
+{
+    if (!out || !opts) return CDC_E_INVALID;
+    *out = nullptr;
+    const int v = cdc_validate(algorithm, opts);
+    if (v != CDC_OK) return v;
+    DeviceCtx *ctx = nullptr;
+    int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    auto *s = new cdc_stream();
+    s->device = device;
+    s->opts = *opts;
+    s->P = make_params(opts);
+    uint64_t w = window_bytes ? window_bytes : (64ull << 20);
+    w = std::max<uint64_t>(w, 2ull * opts->max_size + 4096);
+    s->win = w;
+    s->cuts_cap = w / opts->min_size + 2;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&s->h_win), w, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&s->d_win), w) != hipSuccess ||
+        cdc_device_workspace_size(w, opts, &s->ws_bytes) != CDC_OK ||
+        hipMalloc(&s->d_ws, s->ws_bytes) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&s->d_cuts), s->cuts_cap * sizeof(cdc_cut)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&s->h_cuts), s->cuts_cap * sizeof(cdc_cut),
+                      hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&s->d_res), sizeof(cdc_result)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&s->h_res), sizeof(cdc_result),
+                      hipHostMallocDefault) != hipSuccess) {
+        stream_release(s);
+        return CDC_E_DEVICE;
+    }
+    *out = s;
+    return CDC_OK;
+}
+
+extern "C" int cdc_stream_buffer(cdc_stream *s, uint8_t **write_ptr, uint64_t *space)
+{
+    if (!s || !write_ptr || !space) return CDC_E_INVALID;
+    // drop the bytes of chunks already handed out once every decided chunk was served
+    if (s->ran && s->next_cut >= s->ncuts && s->consumed) {
+        std::memmove(s->h_win, s->h_win + s->consumed, s->fill - s->consumed);
+        s->fill -= s->consumed;
+        s->consumed = 0;
+        s->ncuts = s->next_cut = 0;
+        s->ran = false;
+    }
+    *write_ptr = s->h_win + s->fill;
+    *space = s->win - s->fill;
+    return CDC_OK;
+}
+
+extern "C" int cdc_stream_commit(cdc_stream *s, uint64_t nbytes, int eof)
+{
+    if (!s || nbytes > s->win - s->fill) return CDC_E_INVALID;
+    s->fill += nbytes;
+    if (eof) s->eof = true;
+    return CDC_OK;
+}
+
+static int stream_run(cdc_stream *s)
+{
+    if (hipSetDevice(s->device) != hipSuccess) return CDC_E_DEVICE;
+    HIPCHK(hipMemcpyAsync(s->d_win, s->h_win, s->fill, hipMemcpyHostToDevice, s->stream));
+    const int st = cdc_chunk_device_async(s->device, s->d_win, s->fill, s->eof ? 1 : 0, &s->opts,
+                                          s->d_cuts, s->cuts_cap, s->d_res, s->d_ws, s->ws_bytes,
+                                          s->stream);
+    if (st != CDC_OK) return st;
+    HIPCHK(hipMemcpyAsync(s->h_res, s->d_res, sizeof(cdc_result), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    const cdc_result r = *s->h_res;
+    if (r.status != CDC_OK) return int(r.status);
+    if (r.ncuts)
+        HIPCHK(hipMemcpy(s->h_cuts, s->d_cuts, r.ncuts * sizeof(cdc_cut), hipMemcpyDeviceToHost));
+    s->ncuts = r.ncuts;
+    s->next_cut = 0;
+    s->consumed = s->eof ? s->fill : r.consumed;
+    s->ran = true;
+    return CDC_OK;
+}
+
+extern "C" int cdc_stream_next(cdc_stream *s, const uint8_t **chunk, uint64_t *len)
+{
+    if (!s || !chunk || !len) return CDC_E_INVALID;
+    *chunk = nullptr;
+    *len = 0;
+    for (;;) {
+        if (s->ran && s->next_cut < s->ncuts) {
+            const cdc_cut c = s->h_cuts[s->next_cut++];
+            *chunk = s->h_win + c.offset;
+            *len = c.length;
+            return CDC_OK;
+        }
+        if (s->ran) {
+            // every decided chunk served: drop them from the window
+            std::memmove(s->h_win, s->h_win + s->consumed, s->fill - s->consumed);
+            s->fill -= s->consumed;
+            s->consumed = 0;
+            s->ncuts = s->next_cut = 0;
+            s->ran = false;
+        }
+        if (s->eof && s->fill == 0) return CDC_EOF;
+        if (!s->eof && s->fill < s->win) return CDC_NEED_DATA;
+        const int st = stream_run(s);
+        if (st != CDC_OK) return st;
+    }
+}
+
+extern "C" void cdc_stream_free(cdc_stream *s) { stream_release(s); }
+
+// Pull-model chunker over a read callback.
+struct cdc_chunker {
+    cdc_stream *s = nullptr;
+    cdc_read_fn read = nullptr;
+    void *ctx = nullptr;
+};
+
+extern "C" int cdc_chunker_new(const char *algorithm, cdc_read_fn read, void *ctx,
+                               const cdc_opts *opts, cdc_chunker **out)
+{
+    if (!read || !out) return CDC_E_INVALID;
+    *out = nullptr;
+    cdc_stream *s = nullptr;
+    Global &g = G();
+    if (!g.init) return CDC_E_NOT_INIT;
+    const int st = cdc_stream_new(algorithm, opts, 0, g.devs.front()->device, &s);
+    if (st != CDC_OK) return st;
+    auto *c = new cdc_chunker();
+    c->s = s;
+    c->read = read;
+    c->ctx = ctx;
+    *out = c;
+    return CDC_OK;
+}
+
+extern "C" int cdc_chunker_next(cdc_chunker *c, const uint8_t **chunk, uint64_t *len)
+{
+    if (!c) return CDC_E_INVALID;
+    for (;;) {
+        const int st = cdc_stream_next(c->s, chunk, len);
+        if (st != CDC_NEED_DATA) return st;
+        uint8_t *p = nullptr;
+        uint64_t space = 0;
+        int r = cdc_stream_buffer(c->s, &p, &space);
+        if (r != CDC_OK) return r;
+        while (space > 0) {
+            const int64_t n = c->read(c->ctx, p, space);
+            if (n < 0) return CDC_E_IO;
+            if (n == 0) {
+                r = cdc_stream_commit(c->s, 0, 1);
+                break;
+            }
+            r = cdc_stream_commit(c->s, uint64_t(n), 0);
+            if (r != CDC_OK) return r;
+            p += n;
+            space -= uint64_t(n);
+        }
+        if (r != CDC_OK) return r;
+    }
+}
+
+extern "C" void cdc_chunker_free(cdc_chunker *c)
+{
+    if (!c) return;
+    cdc_stream_free(c->s);
+    delete c;
+}

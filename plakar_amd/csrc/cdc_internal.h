@@ -1,0 +1,84 @@
+// Internal types shared by the HIP kernels (cdc_kernels.hip) and the C-ABI
+// implementation (cdc_api.cpp).  Not part of the public ABI.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "plakar_cdc.h"
+
+namespace cdc {
+
+constexpr int kMaxBufsPerLaunch = 32;   // buffers per launch group (kernel-arg budget)
+constexpr uint32_t kIdxShift = 16;      // candidate-index block = 64 KiB of input
+constexpr uint64_t kIdxBlock = 1ull << kIdxShift;
+constexpr uint32_t kIdxCap = 32;        // u16 entries per index block (one 64-B line)
+constexpr uint32_t kMaxSegs = 16384;    // resolution segments per buffer
+constexpr uint32_t kScanLaneBytes = 4096;                    // bytes hashed+tested per scan lane
+constexpr uint64_t kScanTaskBytes = 64ull * kScanLaneBytes;  // one wave = one scan task
+constexpr uint32_t kScanWavesPerWG = 8;
+constexpr uint32_t kWalkWavesPerWG = 16;
+constexpr uint64_t kUndet = ~0ull;      // "next chunk start not decided by the bytes present"
+
+// Chunker parameters as the kernels use them.
+struct DevParams {
+    uint64_t min_size, normal_size, max_size;
+    uint32_t ms_lo, ms_hi, ml_lo, ml_hi;  // MaskS / MaskL split in 32-bit halves
+    uint32_t cut_adj;                     // 0: cut at i, 1: cut at i + 1
+    uint32_t win;                         // W = highest mask bit + 1 (window length)
+};
+
+struct BufDesc {
+    const uint8_t *data;
+    uint64_t len;
+    cdc_cut *out;
+    uint64_t cap;
+    cdc_result *res;
+    uint32_t seg_base;   // first resolution segment (global numbering)
+    uint32_t nseg;
+    uint32_t blk_base;   // first candidate-index block (global numbering)
+    uint32_t task_base;  // first scan task (global numbering)
+};
+
+struct Batch {
+    uint32_t nbufs;
+    uint32_t final_;
+    uint32_t total_segs, total_blks, total_tasks;
+    uint32_t cap1, cap2;     // per-segment node capacities (speculative / junction walks)
+    uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
+    uint64_t seg;            // resolution segment length in bytes
+    BufDesc b[kMaxBufsPerLaunch];
+};
+
+// Device workspace, carved out of one caller-provided allocation.
+struct Workspace {
+    uint32_t *blk_cnt;   // [total_blks] candidates seen per index block
+    uint16_t *blk_ent;   // [total_blks * kIdxCap] offsets inside the block
+    uint64_t *w1_nodes;  // [total_segs * cap1] speculative chain per segment
+    uint32_t *w1_cnt;    // [total_segs]
+    uint64_t *w2_nodes;  // [total_segs * cap2] junction walk per segment
+    uint32_t *w2_cnt;    // [total_segs]
+    uint32_t *w2_conv;   // [total_segs] local segment the junction walk merged into / kConv*
+    uint32_t *w2_idx;    // [total_segs] index of the merge node in that segment's chain
+    uint64_t *w2_term;   // [total_segs] terminal node when the junction walk ended the chain
+    uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "needs sequential fallback"
+    const uint64_t *gear;  // 256 entries, device copy
+};
+
+constexpr uint32_t kConvNone = 0xFFFFFFFFu;  // entry was already terminal (chain ended earlier)
+constexpr uint32_t kConvTerm = 0xFFFFFFFEu;  // chain ended inside this junction walk
+constexpr uint32_t kConvOvf = 0xFFFFFFFDu;   // junction walk exceeded cap2 nodes
+
+struct Plan {
+    uint64_t seg;
+    uint32_t cap1, cap2;
+    uint32_t total_segs, total_blks, total_tasks;
+    size_t off_blk_cnt, off_blk_ent, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_w2_cnt,
+        off_w2_conv, off_w2_idx, off_w2_term, off_flags, bytes;
+};
+
+// Host-side helpers implemented in cdc_kernels.hip.
+int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan);
+int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream);
+
+}  // namespace cdc

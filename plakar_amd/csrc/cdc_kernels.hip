@@ -1,0 +1,864 @@
+// MI355X (gfx950) content-defined chunking kernels.
+//
+// Replaces the per-byte FastCDC Gear loop of ext go-cdc-chunkers v0.0.8
+// chunkers/fastcdc (*FastCDC).Algorithm and the (*Chunker).Next driver loop
+// consumed at plakar snapshot/backup.go:647-665.  See DESIGN.md for the data
+// layout and the roofline of each kernel.
+//
+// Pipeline per launch group (<= 32 independent buffers):
+//   k_scan      HBM-bound byte scan.  Every lane rolls the Gear fingerprint
+//               over its own 4 KiB run (64-byte warm-up: the masked bits only
+//               depend on the last W <= 64 bytes), tests MaskS at every
+//               position and appends the rare hits to a candidate index of
+//               64-KiB blocks (u16 offsets).
+//   k_walk1     speculative chains: one wave per resolution segment, walking
+//               next() from the segment start (a guess) across the segment.
+//   k_walk2     junctions: one wave per segment walks the TRUE chain from the
+//               previous segment's exit until it meets a speculative chain.
+//   k_emit      one workgroup per buffer: selects the junction walks that lie
+//               on the chain from offset 0, prefix-sums and writes the
+//               (offset, length) cut list.
+//   k_fallback  sequential single-wave walker; runs only when k_emit flags a
+//               buffer it could not resolve (pathological data) or in debug.
+//
+// next(p) is wave-cooperative and decides exactly what the reference decides:
+// the truncated window [p+Min, p+Min+W-1) (fingerprint reset at p+Min) by a
+// 64-lane weighted prefix scan, full-window MaskS hits from the index, and the
+// MaskL region [p+Normal, p+n) by an on-demand raw wave scan.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "cdc_internal.h"
+
+namespace cdc {
+
+static constexpr uint64_t kNoHit = ~0ull;
+static constexpr uint32_t kRawLaneBytes = 256;  // bytes tested per lane per raw-scan block
+static constexpr uint32_t kWarm = 64;           // warm-up bytes (>= W - 1 for any mask)
+static constexpr uint32_t kNtCap = 4096;        // emit: non-trivial junctions per buffer
+
+// ---------------------------------------------------------------------------
+// Gear table in LDS: 256 entries x 32 copies, 256 B per entry.  Lane l reads
+// copy (l & 31), so the 32 lanes of a ds_read_b64 lane group always hit 32
+// distinct bank pairs: conflict-free gathers whatever the data bytes are.
+// Byte address of entry b for this lane = (b << 8) | ((lane & 31) << 3),
+// built from the packed data word by one v_perm_b32.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gear)
+{
+    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) tab[i] = gear[i >> 5];
+}
+
+__device__ __forceinline__ uint64_t lds_gear(const char *tab, uint32_t addr)
+{
+    return *reinterpret_cast<const uint64_t *>(tab + addr);
+}
+
+__device__ __forceinline__ uint32_t gear_addr(uint32_t laneoff, uint32_t word, int k)
+{
+    // v_perm_b32: byte0 <- laneoff.byte0 (sel 4), byte1 <- word.byte(k), bytes 2,3 <- 0 (sel 0x0C)
+    return __builtin_amdgcn_perm(laneoff, word, 0x0C0C0004u | (uint32_t(k & 3) << 8));
+}
+
+__device__ __forceinline__ uint32_t key_of(uint64_t fp, uint32_t mlo, uint32_t mhi)
+{
+    // zero iff (fp & mask) == 0
+    return (uint32_t(fp) & mlo) | (uint32_t(fp >> 32) & mhi);
+}
+
+__device__ __forceinline__ uint32_t word_of(const uint4 &d, int i)
+{
+    return i == 0 ? d.x : i == 1 ? d.y : i == 2 ? d.z : d.w;
+}
+
+// Roll 16 bytes and return the min of the 16 keys (0 iff some position hit).
+__device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, const char *tab,
+                                                uint32_t laneoff, uint32_t mlo, uint32_t mhi)
+{
+    uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        fp = (fp << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+        acc = min(acc, key_of(fp, mlo, mhi));
+    }
+    return acc;
+}
+
+__device__ __forceinline__ void roll16(const uint4 &d, uint64_t &fp, const char *tab,
+                                       uint32_t laneoff)
+{
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        fp = (fp << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+}
+
+// General 16-byte group at absolute address a: positions < fz have fp = 0
+// (the reference resets fp at p+Min), positions in [ts, te) are tested.
+// Returns the first hit (absolute) or kNoHit; fp is advanced over the group.
+__device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp, uint64_t a,
+                                                    uint64_t ts, uint64_t te, uint64_t fz,
+                                                    const char *tab, uint32_t laneoff,
+                                                    uint32_t mlo, uint32_t mhi)
+{
+    uint64_t hit = kNoHit;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t pos = a + k;
+        const uint64_t g = lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+        fp = pos < fz ? 0ull : (fp << 1) + g;
+        if (hit == kNoHit && pos >= ts && pos < te && pos >= fz && key_of(fp, mlo, mhi) == 0)
+            hit = pos;
+    }
+    return hit;
+}
+
+// ---------------------------------------------------------------------------
+// k_scan: full-window MaskS candidates of every byte into the index.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void index_append(uint32_t *cnt, uint16_t *ent, uint64_t pos)
+{
+    const uint64_t blk = pos >> kIdxShift;
+    const uint32_t slot = atomicAdd(&cnt[blk], 1u);
+    if (slot < kIdxCap) ent[blk * kIdxCap + slot] = uint16_t(pos & (kIdxBlock - 1));
+}
+
+__device__ __forceinline__ void scan_group(const uint4 &d, uint64_t &fp, uint64_t ga, uint64_t as,
+                                           uint64_t ae, uint64_t ub, const char *tab,
+                                           uint32_t laneoff, uint32_t mlo, uint32_t mhi,
+                                           uint32_t *cnt, uint16_t *ent)
+{
+    if (ga >= ae) return;
+    if (ga >= as && ga + 16 <= ae) {
+        const uint64_t fp0 = fp;
+        if (roll16_test(d, fp, tab, laneoff, mlo, mhi) == 0) {
+            // rare: record every hit of the group
+            uint64_t f = fp0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                f = (f << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+                if (key_of(f, mlo, mhi) == 0) index_append(cnt, ent, ga + k - ub);
+            }
+        }
+    } else if (ga + 16 <= as) {
+        roll16(d, fp, tab, laneoff);  // warm-up
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t pos = ga + k;
+            fp = (fp << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+            if (pos >= as && pos < ae && key_of(fp, mlo, mhi) == 0)
+                index_append(cnt, ent, pos - ub);
+        }
+    }
+}
+
+__device__ __forceinline__ void load8(uint4 (&d)[8], uint64_t a, uint64_t ae)
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t ga = a + 16u * i;
+        d[i] = ga < ae ? *reinterpret_cast<const uint4 *>(ga) : make_uint4(0, 0, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(kScanWavesPerWG * 64) void k_scan(const Batch B, const DevParams P,
+                                                              const Workspace W)
+{
+    __shared__ uint64_t s_tab[256 * 32];
+    fill_gear_lds(s_tab, W.gear);
+    __syncthreads();
+    const char *tab = reinterpret_cast<const char *>(s_tab);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t laneoff = (lane & 31u) << 3;
+    const uint32_t task = blockIdx.x * kScanWavesPerWG + (threadIdx.x >> 6);
+    if (task >= B.total_tasks) return;
+    uint32_t b = 0;
+    while (b + 1 < B.nbufs && task >= B.b[b + 1].task_base) ++b;
+    const BufDesc &D = B.b[b];
+
+    const uint64_t s = uint64_t(task - D.task_base) * kScanTaskBytes + uint64_t(lane) * kScanLaneBytes;
+    if (s >= D.len) return;
+    const uint64_t e = min(s + kScanLaneBytes, D.len);
+    const uint64_t ub = reinterpret_cast<uint64_t>(D.data);
+    const uint64_t as = ub + s, ae = ub + e;
+    uint64_t a = (ub + (s >= kWarm ? s - kWarm : 0)) & ~15ull;
+    uint32_t *cnt = W.blk_cnt + D.blk_base;
+    uint16_t *ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
+    const uint32_t mlo = P.ms_lo, mhi = P.ms_hi;
+
+    uint64_t fp = 0;
+    uint4 x[8], y[8];
+    load8(x, a, ae);
+    // double-buffered 128-byte batches per lane: load batch i+1, roll batch i
+    while (a < ae) {
+        load8(y, a + 128, ae);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            scan_group(x[i], fp, a + 16u * i, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
+        a += 128;
+        if (a >= ae) break;
+        load8(x, a + 128, ae);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            scan_group(y[i], fp, a + 16u * i, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
+        a += 128;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative next(p).
+// ---------------------------------------------------------------------------
+struct WalkCtx {
+    uint64_t ub;       // absolute address of byte 0
+    uint64_t len;
+    uint32_t final_;
+    const uint32_t *cnt;
+    const uint16_t *ent;
+    const char *tab;
+    uint32_t laneoff;
+    uint32_t lane;
+};
+
+// First position in [lo, hi) whose fingerprint (reset to 0 before fz) hits the
+// mask, by a raw scan: lane j rolls its own 256-byte slice of a 16-KiB block
+// after a 64-byte warm-up.  Positions are buffer-relative.
+__device__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
+                                  uint32_t mlo, uint32_t mhi)
+{
+    const uint64_t H = C.ub + hi, FZ = C.ub + fz;
+    uint64_t x = C.ub + lo;
+    while (x < H) {
+        const uint64_t A = x & ~15ull;
+        const uint64_t bend = min(A + 64ull * kRawLaneBytes, H);
+        const uint64_t ts = max(x, A + uint64_t(C.lane) * kRawLaneBytes);
+        const uint64_t te = min(bend, A + uint64_t(C.lane + 1) * kRawLaneBytes);
+        uint64_t hit = kNoHit;
+        if (ts < te) {
+            const uint64_t hs = ts >= FZ + kWarm ? ts - kWarm : FZ;
+            uint64_t fp = 0;
+            for (uint64_t a = hs & ~15ull; a < te; a += 16) {
+                const uint4 d = *reinterpret_cast<const uint4 *>(a);
+                if (a >= FZ && a >= ts && a + 16 <= te) {
+                    const uint64_t fp0 = fp;
+                    if (roll16_test(d, fp, C.tab, C.laneoff, mlo, mhi) == 0) {
+                        uint64_t f = fp0;
+                        hit = group_first_hit(d, f, a, ts, te, FZ, C.tab, C.laneoff, mlo, mhi);
+                        break;
+                    }
+                } else if (a >= FZ && a + 16 <= ts) {
+                    roll16(d, fp, C.tab, C.laneoff);
+                } else {
+                    hit = group_first_hit(d, fp, a, ts, te, FZ, C.tab, C.laneoff, mlo, mhi);
+                    if (hit != kNoHit) break;
+                }
+            }
+        }
+        const uint64_t m = __ballot(hit != kNoHit);
+        if (m) return __shfl(hit, __ffsll((unsigned long long)m) - 1) - C.ub;
+        x = bend;
+    }
+    return kNoHit;
+}
+
+// Truncated window: positions fz + j, j < W - 1, fingerprint started at 0 at
+// fz.  fp_j = sum_{k<=j} G[b_k] << (j-k): a weighted inclusive scan over lanes.
+__device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64_t fz,
+                                    uint64_t norm_end, uint64_t lim)
+{
+    const uint32_t j = C.lane;
+    const uint64_t pos = fz + j;
+    const bool valid = (j + 1 < P.win) && pos < lim;
+    uint64_t v = 0;
+    if (valid) {
+        const uint32_t byte = reinterpret_cast<const uint8_t *>(C.ub)[pos];
+        v = lds_gear(C.tab, (byte << 8) | C.laneoff);
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d);
+        if (j >= uint32_t(d)) v += t << d;
+    }
+    const bool small = pos < norm_end;
+    const uint32_t mlo = small ? P.ms_lo : P.ml_lo, mhi = small ? P.ms_hi : P.ml_hi;
+    const uint64_t m = __ballot(valid && key_of(v, mlo, mhi) == 0);
+    return m ? fz + uint64_t(__ffsll((unsigned long long)m) - 1) : kNoHit;
+}
+
+// First full-window MaskS candidate in [a, b), from the index.  Index blocks
+// that overflowed (dense data) are rescanned raw.
+__device__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+                                    uint64_t fz)
+{
+    const uint64_t blk0 = a >> kIdxShift, blk1 = (b - 1) >> kIdxShift;
+    for (uint64_t base = blk0; base <= blk1; base += 64) {
+        const uint64_t blk = base + C.lane;
+        const bool in = blk <= blk1;
+        const uint32_t c = in ? C.cnt[blk] : 0u;
+        const bool dense = in && c > kIdxCap;
+        uint64_t best = kNoHit;
+        if (in && !dense) {
+            const uint64_t bstart = blk << kIdxShift;
+            const uint16_t *e = C.ent + blk * kIdxCap;
+            for (uint32_t i = 0; i < c; ++i) {
+                const uint64_t pos = bstart + e[i];
+                if (pos >= a && pos < b && pos < best) best = pos;
+            }
+        }
+        uint64_t found = __ballot(best != kNoHit);
+        uint64_t dn = __ballot(dense);
+        while (found | dn) {
+            const int lf = found ? __ffsll((unsigned long long)found) - 1 : 64;
+            const int ld = dn ? __ffsll((unsigned long long)dn) - 1 : 64;
+            if (lf < ld) return __shfl(best, lf);
+            const uint64_t db = base + uint64_t(ld);
+            const uint64_t lo = max(a, db << kIdxShift), hi = min(b, (db + 1) << kIdxShift);
+            const uint64_t h = raw_first_hit(C, lo, hi, fz, P.ms_lo, P.ms_hi);
+            if (h != kNoHit) return h;
+            dn &= ~(1ull << ld);
+        }
+    }
+    return kNoHit;
+}
+
+// The reference's (*Chunker).Next + (*FastCDC).Algorithm for the chunk that
+// starts at p: returns the next chunk start, len at the end of a final
+// stream, or kUndet when the bytes present do not decide the cut.
+__device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
+{
+    const uint64_t E = C.len, r = E - p;
+    if (r <= P.min_size) return C.final_ ? E : kUndet;
+    uint64_t n, norm = P.normal_size, lim;
+    bool clipped = false;
+    if (C.final_) {
+        if (r >= P.max_size) {
+            n = P.max_size;
+        } else {
+            n = r;
+            if (r <= P.normal_size) norm = r;
+        }
+        lim = p + n;
+    } else {
+        n = P.max_size;  // more stream follows: the reference peeks a full MaxSize window
+        lim = p + n;
+        if (lim > E) {
+            lim = E;
+            clipped = true;
+        }
+    }
+    const uint64_t fz = p + P.min_size;
+    const uint64_t norm_end = p + norm;
+    uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim);
+    if (h != kNoHit) return h + P.cut_adj;
+    const uint64_t full0 = fz + (P.win - 1);
+    const uint64_t s_end = min(norm_end, lim);
+    if (full0 < s_end) {
+        h = index_first_hit(C, P, full0, s_end, fz);
+        if (h != kNoHit) return h + P.cut_adj;
+    }
+    const uint64_t l_lo = max(norm_end, full0);
+    if (l_lo < lim) {
+        h = raw_first_hit(C, l_lo, lim, fz, P.ml_lo, P.ml_hi);
+        if (h != kNoHit) return h + P.cut_adj;
+    }
+    return clipped ? kUndet : p + n;
+}
+
+__device__ __forceinline__ uint32_t buf_of_seg(const Batch &B, uint32_t g)
+{
+    uint32_t b = 0;
+    while (b + 1 < B.nbufs && g >= B.b[b + 1].seg_base) ++b;
+    return b;
+}
+
+__device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, const Workspace &W,
+                                            const char *tab)
+{
+    WalkCtx C;
+    C.ub = reinterpret_cast<uint64_t>(D.data);
+    C.len = D.len;
+    C.final_ = B.final_;
+    C.cnt = W.blk_cnt + D.blk_base;
+    C.ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
+    C.tab = tab;
+    C.lane = threadIdx.x & 63u;
+    C.laneoff = (C.lane & 31u) << 3;
+    return C;
+}
+
+// ---------------------------------------------------------------------------
+// k_walk1: speculative chain per segment, started at the segment start.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, const DevParams P,
+                                                               const Workspace W)
+{
+    __shared__ uint64_t s_tab[256 * 32];
+    fill_gear_lds(s_tab, W.gear);
+    __syncthreads();
+    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
+    if (g >= B.total_segs) return;
+    const uint32_t b = buf_of_seg(B, g);
+    const BufDesc &D = B.b[b];
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    const uint64_t q = g - D.seg_base;
+    const uint64_t seg_end = (q + 1) * B.seg;
+    uint64_t *nodes = W.w1_nodes + size_t(g) * B.cap1;
+    uint64_t p = q * B.seg;
+    uint32_t c = 0;
+    if (C.lane == 0) nodes[c] = p;
+    ++c;
+    for (;;) {
+        const uint64_t nx = next_node(C, P, p);
+        if (C.lane == 0) nodes[c] = nx;
+        ++c;
+        if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) break;
+        p = nx;
+    }
+    if (C.lane == 0) W.w1_cnt[g] = c;
+}
+
+// ---------------------------------------------------------------------------
+// k_walk2: junction walk from the previous segment's exit until the chain
+// meets a node of some segment's speculative chain.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, const DevParams P,
+                                                               const Workspace W)
+{
+    __shared__ uint64_t s_tab[256 * 32];
+    fill_gear_lds(s_tab, W.gear);
+    __syncthreads();
+    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
+    if (g >= B.total_segs) return;
+    const uint32_t b = buf_of_seg(B, g);
+    const BufDesc &D = B.b[b];
+    if (g == D.seg_base) return;  // segment 0 of a buffer has no junction
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    const uint32_t cap1 = B.cap1;
+    const uint64_t e = W.w1_nodes[size_t(g - 1) * cap1 + W.w1_cnt[g - 1] - 1];
+    uint32_t conv = kConvNone, idx = 0, c2 = 0;
+    uint64_t term = e;
+    uint64_t *out = W.w2_nodes + size_t(g) * B.cap2;
+    if (e != kUndet && e < C.len) {
+        uint64_t x = e;
+        for (;;) {
+            const uint64_t s = x / B.seg;
+            const uint32_t gs = D.seg_base + uint32_t(s);
+            const uint32_t ns = W.w1_cnt[gs] - 1;  // speculative nodes below the segment exit
+            const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
+            int k = -1;
+            for (uint32_t base = 0; base < ns && k < 0; base += 64) {
+                const uint32_t i = base + C.lane;
+                const uint64_t m = __ballot(i < ns && sn[i] == x);
+                if (m) k = int(base) + __ffsll((unsigned long long)m) - 1;
+            }
+            if (k >= 0) {
+                conv = uint32_t(s);
+                idx = uint32_t(k);
+                break;
+            }
+            if (c2 >= B.cap2) {
+                conv = kConvOvf;
+                break;
+            }
+            if (C.lane == 0) out[c2] = x;
+            ++c2;
+            x = next_node(C, P, x);
+            if (x == kUndet || x >= C.len) {
+                conv = kConvTerm;
+                term = x;
+                break;
+            }
+        }
+    }
+    if (C.lane == 0) {
+        W.w2_conv[g] = conv;
+        W.w2_idx[g] = idx;
+        W.w2_cnt[g] = c2;
+        W.w2_term[g] = term;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_emit: one workgroup per buffer.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum, uint32_t &total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d);
+        if (lane >= uint32_t(d)) incl += t;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t x = s_wsum[w];
+        if (w < wave) off += x;
+        tot += x;
+    }
+    __syncthreads();
+    total = tot;
+    return off + incl - v;
+}
+
+__global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
+{
+    __shared__ uint32_t s_nt[kNtCap];
+    __shared__ uint32_t s_ivs[kNtCap], s_ive[kNtCap];
+    __shared__ uint32_t s_wsum[16];
+    __shared__ uint32_t s_m, s_niv, s_fail;
+
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const BufDesc &D = B.b[b];
+    const uint32_t NS = D.nseg, G0 = D.seg_base, cap1 = B.cap1, cap2 = B.cap2;
+    const uint64_t len = D.len;
+    if (NS == 0) {
+        if (tid == 0) {
+            W.flags[b] = 0;
+            D.res->ncuts = 0;
+            D.res->consumed = 0;
+            D.res->status = CDC_OK;
+            D.res->needed = 0;
+        }
+        return;
+    }
+    if (B.force_fallback) {
+        if (tid == 0) W.flags[b] = 1;
+        return;
+    }
+    const uint64_t e0 = W.w1_nodes[size_t(G0) * cap1 + W.w1_cnt[G0] - 1];
+    const bool cont = NS > 1 && e0 != kUndet && e0 < len;
+
+    // Phase 1: compact the junctions that do not simply hand over to the next segment.
+    if (tid == 0) {
+        s_m = 0;
+        s_fail = 0;
+        s_niv = 0;
+    }
+    __syncthreads();
+    if (cont) {
+        for (uint32_t base = 1; base < NS; base += blockDim.x) {
+            const uint32_t q = base + tid;
+            bool nt = false;
+            if (q < NS) {
+                const uint32_t c = W.w2_conv[G0 + q];
+                nt = c >= kConvOvf || c != q;  // jump = c + 1 differs from q + 1
+            }
+            uint32_t tot;
+            const uint32_t pre = block_excl_scan(nt ? 1u : 0u, s_wsum, tot);
+            const uint32_t m0 = s_m;
+            if (nt && m0 + pre < kNtCap) s_nt[m0 + pre] = q;
+            __syncthreads();
+            if (tid == 0) s_m = m0 + tot;
+            __syncthreads();
+        }
+    }
+    // Phase 2: follow the chain from segment 1 over the non-trivial junctions.
+    if (tid == 0 && cont) {
+        const uint32_t m = s_m;
+        uint32_t niv = 0, fail = 0, cur = 1;
+        if (m > kNtCap) {
+            fail = 1;
+        } else {
+            for (uint32_t i = 0; i < m; ++i) {
+                const uint32_t p = s_nt[i];
+                if (p < cur) continue;  // skipped by an earlier junction walk
+                const uint32_t c = W.w2_conv[G0 + p];
+                if (c == kConvOvf) {
+                    fail = 1;
+                    break;
+                }
+                const uint32_t j = c >= kConvOvf ? NS : c + 1;
+                if (j > p + 1) {
+                    s_ivs[niv] = p + 1;
+                    s_ive[niv] = j;
+                    ++niv;
+                }
+                cur = j;
+                if (cur >= NS) break;
+            }
+        }
+        s_niv = niv;
+        s_fail = fail;
+    }
+    __syncthreads();
+    if (s_fail) {
+        if (tid == 0) W.flags[b] = 1;
+        return;
+    }
+    const uint32_t niv = s_niv;
+
+    // Phase 3: per-piece node counts, prefix sum, write cuts.
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < NS; base += blockDim.x) {
+        const uint32_t q = base + tid;
+        bool valid = false;
+        if (q < NS) {
+            if (q == 0) {
+                valid = true;
+            } else if (cont) {
+                // binary search: last interval with start <= q
+                int lo = 0, hi = int(niv) - 1, f = -1;
+                while (lo <= hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_ivs[mid] <= q) {
+                        f = mid;
+                        lo = mid + 1;
+                    } else {
+                        hi = mid - 1;
+                    }
+                }
+                valid = !(f >= 0 && q < s_ive[f]);
+            }
+        }
+        uint32_t c2 = 0, cnt = 0, k = 0, gs = 0;
+        uint64_t end = 0;
+        const uint64_t *list2 = nullptr;
+        if (valid) {
+            if (q == 0) {
+                cnt = W.w1_cnt[G0] - 1;
+                gs = G0;
+                k = 0;
+                end = e0;
+            } else {
+                const uint32_t c = W.w2_conv[G0 + q];
+                c2 = W.w2_cnt[G0 + q];
+                list2 = W.w2_nodes + size_t(G0 + q) * cap2;
+                if (c < kConvOvf) {
+                    gs = G0 + c;
+                    k = W.w2_idx[G0 + q];
+                    const uint32_t n1 = W.w1_cnt[gs];
+                    cnt = c2 + (n1 - 1 - k);
+                    end = W.w1_nodes[size_t(gs) * cap1 + n1 - 1];
+                } else if (c == kConvTerm) {
+                    cnt = c2;
+                    end = W.w2_term[G0 + q];
+                } else {
+                    cnt = 0;  // chain ended before this segment
+                }
+            }
+        }
+        const uint32_t emit = cnt - ((cnt > 0 && end == kUndet) ? 1u : 0u);
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan(emit, s_wsum, tot);
+        if (cnt > 0) {
+            const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
+            uint64_t idx = uint64_t(carry) + pre;
+            for (uint32_t t = 0; t < cnt; ++t) {
+                const uint64_t pos = t < c2 ? list2[t] : sn[k + (t - c2)];
+                const uint64_t succ =
+                    t + 1 < cnt ? (t + 1 < c2 ? list2[t + 1] : sn[k + (t + 1 - c2)]) : end;
+                if (succ == kUndet) {
+                    D.res->consumed = pos;  // the last chunk is not decided yet
+                    break;
+                }
+                if (idx < D.cap) {
+                    cdc_cut cut;
+                    cut.offset = pos;
+                    cut.length = uint32_t(succ - pos);
+                    cut.reserved = 0;
+                    D.out[idx] = cut;
+                }
+                ++idx;
+                if (succ >= len) D.res->consumed = len;
+            }
+        }
+        carry += tot;
+    }
+    if (tid == 0) {
+        W.flags[b] = 0;
+        D.res->ncuts = carry <= D.cap ? carry : D.cap;
+        D.res->status = carry <= D.cap ? CDC_OK : CDC_E_NOSPACE;
+        D.res->needed = carry;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fallback: sequential single-wave resolver (same next() as above).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_fallback(const Batch B, const DevParams P,
+                                                 const Workspace W)
+{
+    const uint32_t b = blockIdx.x;
+    if (W.flags[b] == 0) return;
+    __shared__ uint64_t s_tab[256 * 32];
+    fill_gear_lds(s_tab, W.gear);
+    __syncthreads();
+    const BufDesc &D = B.b[b];
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    uint64_t p = 0, idx = 0;
+    while (p < C.len) {
+        const uint64_t nx = next_node(C, P, p);
+        if (nx == kUndet) break;
+        if (C.lane == 0 && idx < D.cap) {
+            cdc_cut cut;
+            cut.offset = p;
+            cut.length = uint32_t(nx - p);
+            cut.reserved = 0;
+            D.out[idx] = cut;
+        }
+        ++idx;
+        p = nx;
+    }
+    if (C.lane == 0) {
+        D.res->ncuts = idx <= D.cap ? idx : D.cap;
+        D.res->consumed = p;
+        D.res->status = idx <= D.cap ? CDC_OK : CDC_E_NOSPACE;
+        D.res->needed = idx;
+        W.flags[b] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side: planning and launching.
+// ---------------------------------------------------------------------------
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
+{
+    uint64_t maxlen = 0;
+    for (int i = 0; i < nbufs; ++i) maxlen = lens[i] > maxlen ? lens[i] : maxlen;
+    uint64_t mult = 8;
+    if (const char *env = getenv("CDC_SEG_MULT")) {
+        const long v = atol(env);
+        if (v >= 2 && v <= 1024) mult = uint64_t(v);
+    }
+    uint64_t seg = mult * P.min_size;
+    const uint64_t need = (maxlen + kMaxSegs - 1) / kMaxSegs;
+    if (seg < need) seg = need;
+    seg = (seg + 15) & ~15ull;
+    plan->seg = seg;
+    plan->cap1 = uint32_t(seg / P.min_size + 3);
+    plan->cap2 = 4 * plan->cap1 + 16;
+    uint64_t segs = 0, blks = 0, tasks = 0;
+    for (int i = 0; i < nbufs; ++i) {
+        segs += (lens[i] + seg - 1) / seg;
+        blks += (lens[i] + kIdxBlock - 1) / kIdxBlock;
+        tasks += (lens[i] + kScanTaskBytes - 1) / kScanTaskBytes;
+    }
+    if (segs >= 0xFFFF0000ull || blks >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
+    plan->total_segs = uint32_t(segs);
+    plan->total_blks = uint32_t(blks);
+    plan->total_tasks = uint32_t(tasks);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = align_up(off + bytes, 256);
+        return o;
+    };
+    plan->off_blk_cnt = take(blks * 4);
+    plan->off_blk_ent = take(blks * kIdxCap * 2);
+    plan->off_w1_nodes = take(segs * plan->cap1 * 8);
+    plan->off_w1_cnt = take(segs * 4);
+    plan->off_w2_nodes = take(segs * plan->cap2 * 8);
+    plan->off_w2_cnt = take(segs * 4);
+    plan->off_w2_conv = take(segs * 4);
+    plan->off_w2_idx = take(segs * 4);
+    plan->off_w2_term = take(segs * 8);
+    plan->off_flags = take(kMaxBufsPerLaunch * 4);
+    plan->bytes = off;
+    return CDC_OK;
+}
+
+// Optional live profiling: hipEvents recorded on the launch stream around the
+// scan kernel and around the whole pipeline of each launch group.
+struct ProfRec {
+    hipEvent_t e0, e1, e2;  // before k_scan, after k_scan, after k_fallback
+    uint64_t scan_bytes;
+};
+static std::mutex g_prof_mu;
+static bool g_prof_on = false;
+static std::vector<ProfRec> g_prof_live, g_prof_pool;
+
+static bool prof_begin(ProfRec &r, uint64_t bytes)
+{
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (!g_prof_on) return false;
+    if (!g_prof_pool.empty()) {
+        r = g_prof_pool.back();
+        g_prof_pool.pop_back();
+    } else if (hipEventCreate(&r.e0) != hipSuccess || hipEventCreate(&r.e1) != hipSuccess ||
+               hipEventCreate(&r.e2) != hipSuccess) {
+        return false;
+    }
+    r.scan_bytes = bytes;
+    return true;
+}
+
+int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream)
+{
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (B.nbufs == 0) return CDC_OK;
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < B.nbufs; ++i) bytes += B.b[i].len;
+    ProfRec pr;
+    const bool prof = prof_begin(pr, bytes);
+    if (B.total_blks > 0 &&
+        hipMemsetAsync(W.blk_cnt, 0, size_t(B.total_blks) * 4, st) != hipSuccess)
+        return CDC_E_DEVICE;
+    if (prof) (void)hipEventRecord(pr.e0, st);
+    if (B.total_tasks > 0)
+        hipLaunchKernelGGL(k_scan, dim3((B.total_tasks + kScanWavesPerWG - 1) / kScanWavesPerWG),
+                           dim3(kScanWavesPerWG * 64), 0, st, B, P, W);
+    if (prof) (void)hipEventRecord(pr.e1, st);
+    if (B.total_segs > 0 && !B.force_fallback) {
+        const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
+        hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
+        hipLaunchKernelGGL(k_walk2, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
+    }
+    hipLaunchKernelGGL(k_emit, dim3(B.nbufs), dim3(1024), 0, st, B, W);
+    hipLaunchKernelGGL(k_fallback, dim3(B.nbufs), dim3(64), 0, st, B, P, W);
+    if (prof) {
+        (void)hipEventRecord(pr.e2, st);
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof_live.push_back(pr);
+    }
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+}
+
+}  // namespace cdc
+
+extern "C" int cdc_profile_enable(int on)
+{
+    std::lock_guard<std::mutex> lk(cdc::g_prof_mu);
+    cdc::g_prof_on = on != 0;
+    return CDC_OK;
+}
+
+extern "C" int cdc_profile_collect(double *scan_ms, double *pipeline_ms, uint64_t *launches,
+                                   uint64_t *scan_bytes)
+{
+    std::vector<cdc::ProfRec> recs;
+    {
+        std::lock_guard<std::mutex> lk(cdc::g_prof_mu);
+        recs.swap(cdc::g_prof_live);
+    }
+    double s = 0, t = 0;
+    uint64_t bytes = 0;
+    int st = CDC_OK;
+    for (auto &r : recs) {
+        float a = 0, b = 0;
+        if (hipEventSynchronize(r.e2) != hipSuccess || hipEventElapsedTime(&a, r.e0, r.e1) != hipSuccess ||
+            hipEventElapsedTime(&b, r.e0, r.e2) != hipSuccess)
+            st = CDC_E_DEVICE;
+        s += a;
+        t += b;
+        bytes += r.scan_bytes;
+    }
+    {
+        std::lock_guard<std::mutex> lk(cdc::g_prof_mu);
+        for (auto &r : recs) cdc::g_prof_pool.push_back(r);
+    }
+    if (scan_ms) *scan_ms = s;
+    if (pipeline_ms) *pipeline_ms = t;
+    if (launches) *launches = recs.size();
+    if (scan_bytes) *scan_bytes = bytes;
+    return st;
+}
+
+namespace cdc {
+
+}  // namespace cdc

@@ -1,0 +1,293 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle, bit-exact.
+
+Every test here runs the product library on an MI355X and compares its cut
+lists with oracle/fastcdc_oracle.c on the same bytes.  PARITY UNPINNED w.r.t.
+the Go module: the oracle is a restatement, pinned by the
+committed golden vectors in tests/golden/.
+"""
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from datagen import gear_table, low_entropy, random_bytes, zipf_sizes  # noqa: E402
+from oracle_ref import DEFAULT_MASK_L, DEFAULT_MASK_S  # noqa: E402
+from plakar_amd import _lib, chunkers, device, repository  # noqa: E402
+from plakar_amd.chunking import Configuration, DefaultConfiguration  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEF = dict(min_size=65536, normal_size=1 << 20, max_size=4 << 20)
+
+
+def _placeholder():
+    return _lib.default_gear()
+
+
+def _opts(p):
+    return chunkers.ChunkerOpts(MinSize=p["min_size"], NormalSize=p["normal_size"], MaxSize=p["max_size"])
+
+
+def gpu_chunk(arrays, p, gear=None, cut_adj=0, final=True, offsets=None):
+    """Chunk host numpy arrays on the GPU via the device path; returns a list of
+    uint64 (n, 2) arrays."""
+    _lib.ensure_init(gear=gear, cut_convention=cut_adj)
+    ts = []
+    for i, a in enumerate(arrays):
+        off = 0 if offsets is None else offsets[i]
+        t = torch.empty(a.size + off + 16, dtype=torch.uint8, device="cuda")
+        t[off:off + a.size].copy_(torch.from_numpy(np.ascontiguousarray(a)))
+        ts.append(t[off:off + a.size])
+    b = device.DeviceBatch(ts, _opts(p), final=final)
+    b.launch()
+    cuts, res = b.results()
+    return [c.cpu().numpy().astype(np.uint64) for c in cuts], res
+
+
+def assert_same(got, ref, what=""):
+    assert got.shape == ref.shape, f"{what}: {got.shape[0]} chunks vs oracle {ref.shape[0]}"
+    bad = np.nonzero((got != ref).any(axis=1))[0]
+    assert bad.size == 0, f"{what}: first mismatch at chunk {bad[0]}: {got[bad[0]]} vs {ref[bad[0]]}"
+
+
+@pytest.fixture(autouse=True)
+def _reset_debug():
+    device.set_debug_mode(0)
+    yield
+    device.set_debug_mode(0)
+    _lib.ensure_init()
+
+
+# ---------------------------------------------------------------- golden vectors
+def _golden_cases():
+    with open(os.path.join(GOLDEN, "golden_vectors.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _golden_cases(), ids=lambda c: c["name"])
+def test_device_matches_golden(oracle, case):
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden as mg
+    data = mg.make_input(case["input"])
+    gear = mg.gear_for(case["gear"])
+    (got,), _ = gpu_chunk([data], case["params"], gear=gear, cut_adj=case["cut_adj"])
+    assert [int(x) for x in got[:, 1]] == case["lengths"]
+    assert int(got[:, 1].sum()) == data.size
+
+
+# ---------------------------------------------------------------- parameter sweep
+PARAMS = [
+    dict(min_size=64, normal_size=256, max_size=1024),
+    dict(min_size=64, normal_size=100, max_size=130),
+    dict(min_size=2048, normal_size=8192, max_size=65536),
+    dict(min_size=4096, normal_size=16384, max_size=20000),
+    DEF,
+]
+
+
+@pytest.mark.parametrize("p", PARAMS, ids=lambda p: f"{p['min_size']}-{p['normal_size']}-{p['max_size']}")
+@pytest.mark.parametrize("kind", ["random", "low_entropy", "zeros", "mixed"])
+@pytest.mark.parametrize("cut_adj", [0, 1])
+def test_device_param_sweep(oracle, p, kind, cut_adj):
+    n = 3 << 20
+    if kind == "random":
+        data = random_bytes(n, 21)
+    elif kind == "low_entropy":
+        data = low_entropy(n, 22, 0.01)
+    elif kind == "zeros":
+        data = np.zeros(n, np.uint8)
+    else:
+        data = np.concatenate([random_bytes(n // 3, 23), np.zeros(n // 3, np.uint8), low_entropy(n // 3, 24, 0.002)])
+    gear = gear_table(31)
+    (got,), _ = gpu_chunk([data], p, gear=gear, cut_adj=cut_adj)
+    assert_same(got, oracle.chunk(data, gear, cut_adj=cut_adj, **p), f"{kind}")
+
+
+@pytest.mark.parametrize("size", [0, 1, 63, 64, 65, 1000, 65535, 65536, 65537, 65536 + 49, 1 << 20, (4 << 20) + 1, 9_999_999])
+def test_device_sizes(oracle, size):
+    data = random_bytes(size, size)
+    gear = _placeholder()
+    (got,), res = gpu_chunk([data], DEF, gear=gear)
+    ref = oracle.chunk(data, gear, **DEF)
+    assert_same(got, ref, f"size {size}")
+    assert int(res[0, 1]) == size  # consumed
+
+
+@pytest.mark.parametrize("off", [1, 3, 7, 8, 13, 15])
+def test_device_unaligned(oracle, off):
+    p = dict(min_size=2048, normal_size=8192, max_size=65536)
+    data = random_bytes((1 << 20) + off * 7, off)
+    gear = gear_table(off)
+    (got,), _ = gpu_chunk([data], p, gear=gear, offsets=[off])
+    assert_same(got, oracle.chunk(data, gear, **p), f"offset {off}")
+
+
+def test_device_dense_candidates(oracle):
+    """G[0] = 0: every all-zero window hits MaskS, so every index block
+    overflows and the chains never merge (offset-preserving): exercises the
+    dense raw rescans and the sequential fallback resolver."""
+    gear = gear_table(40)
+    gear[0] = 0
+    data = np.concatenate([np.zeros(24 << 20, np.uint8), random_bytes(8 << 20, 41)])
+    (got,), _ = gpu_chunk([data], DEF, gear=gear)
+    assert_same(got, oracle.chunk(data, gear, **DEF), "dense")
+
+
+def test_device_alternative_masks(oracle):
+    """Masks are runtime parameters (v0.0.8 values unverified)."""
+    ms, ml = 0x0000000000001FFF, 0x00000000000001FF   # low bits: W = 13
+    _lib.ensure_init(gear=gear_table(50), mask_s=ms, mask_l=ml)
+    data = random_bytes(2 << 20, 50)
+    t = torch.from_numpy(data).cuda()
+    p = dict(min_size=1024, normal_size=8192, max_size=32768)
+    b = device.DeviceBatch([t], _opts(p))
+    b.launch()
+    (c,), _ = b.results()
+    got = c.cpu().numpy().astype(np.uint64)
+    assert_same(got, oracle.chunk(data, gear_table(50), mask_s=ms, mask_l=ml, **p), "masks")
+
+
+# ---------------------------------------------------------------- debug resolver
+@pytest.mark.parametrize("kind", ["random", "low_entropy"])
+def test_sequential_resolver_matches(oracle, kind):
+    data = random_bytes(16 << 20, 60) if kind == "random" else low_entropy(16 << 20, 61)
+    gear = _placeholder()
+    device.set_debug_mode(1)
+    (got,), _ = gpu_chunk([data], DEF, gear=gear)
+    device.set_debug_mode(0)
+    assert_same(got, oracle.chunk(data, gear, **DEF), "sequential")
+
+
+# ---------------------------------------------------------------- streaming windows
+@pytest.mark.parametrize("window", [(4 << 20) + 4096, 9 << 20, 33 << 20])
+def test_nonfinal_windows_compose(oracle, window):
+    """final = 0 windows + resume at `consumed` == the whole stream (the
+    Peek(MaxSize) carry of ext chunker.go)."""
+    data = np.concatenate([random_bytes(40 << 20, 70), low_entropy(20 << 20, 71)])
+    gear = _placeholder()
+    ref = oracle.chunk(data, gear, **DEF)
+    got, off = [], 0
+    while off < data.size:
+        w = min(window, data.size - off)
+        fin = off + w == data.size
+        (c,), res = gpu_chunk([data[off:off + w]], DEF, gear=gear, final=fin)
+        c = c.copy()
+        c[:, 0] += np.uint64(off)
+        got.append(c)
+        consumed = int(res[0, 1])
+        assert fin or consumed > 0
+        off = off + w if fin else off + consumed
+    assert_same(np.concatenate(got), ref, f"window {window}")
+
+
+# ---------------------------------------------------------------- batched buffers
+def test_batch_many_buffers(oracle):
+    """Independent buffers in one launch group (and more than one group)."""
+    p = dict(min_size=2048, normal_size=8192, max_size=65536)
+    sizes = [0, 5, 2047, 2048, 70000, 1 << 20, 3 << 20] * 6
+    arrays = [random_bytes(s, 80 + i) if i % 3 else low_entropy(s, 80 + i) for i, s in enumerate(sizes)]
+    gear = gear_table(81)
+    got, res = gpu_chunk(arrays, p, gear=gear)
+    for i, a in enumerate(arrays):
+        assert_same(got[i], oracle.chunk(a, gear, **p), f"buffer {i} ({a.size} B)")
+
+
+def test_c2_shape_32x64MiB(oracle):
+    """BASELINE configs[2], one GPU's share: 32 x 64 MiB random buffers."""
+    arrays = [random_bytes(64 << 20, 100 + i) for i in range(32)]
+    gear = _placeholder()
+    got, _ = gpu_chunk(arrays, DEF, gear=gear)
+    for i, a in enumerate(arrays):
+        assert_same(got[i], oracle.chunk(a, gear, **DEF), f"buffer {i}")
+
+
+def test_c1_full_1GiB(oracle):
+    """BASELINE configs[1]: 1 GiB random, default params, bit-exact."""
+    data = random_bytes(1 << 30, 1)
+    gear = _placeholder()
+    (got,), _ = gpu_chunk([data], DEF, gear=gear)
+    assert_same(got, oracle.chunk(data, gear, **DEF), "C1")
+
+
+def test_c3_low_entropy_1GiB(oracle):
+    """BASELINE configs[3], one GPU's share: 1 GiB zeros + 1 % random bytes."""
+    data = low_entropy(1 << 30, 200)
+    gear = _placeholder()
+    (got,), _ = gpu_chunk([data], DEF, gear=gear)
+    assert_same(got, oracle.chunk(data, gear, **DEF), "C3")
+
+
+# ---------------------------------------------------------------- host paths / Go API mirror
+def test_chunk_buffers_host_path(oracle, monkeypatch):
+    """cdc_chunk: host buffers in, host lists out; includes a buffer larger
+    than the staging arena (streamed through it)."""
+    monkeypatch.setenv("CDC_HOST_ARENA_MB", "16")
+    _lib.ensure_init()
+    arrays = [random_bytes(s, 90 + i) for i, s in enumerate([0, 100, 65536, 70000, 5 << 20, 40 << 20, 1 << 20])]
+    gear = _placeholder()
+    res = chunkers.ChunkBuffers(arrays, _opts(DEF))
+    for i, a in enumerate(arrays):
+        assert_same(res[i], oracle.chunk(a, gear, **DEF), f"host buffer {i}")
+
+
+def test_chunker_next_mirror(oracle):
+    """chunkers.NewChunker("fastcdc", rd, opts) + Next() until EOF."""
+    _lib.ensure_init()
+    data = np.concatenate([random_bytes(150 << 20, 95), low_entropy(30 << 20, 96)])
+    chk = chunkers.NewChunker("fastcdc", io.BytesIO(data.tobytes()), _opts(DEF))
+    lens = []
+    while True:
+        chunk, err = chk.Next()
+        if err is chunkers.EOF:
+            assert chunk is None
+            break
+        lens.append(len(chunk))
+    ref = oracle.chunk(data, _placeholder(), **DEF)
+    assert lens == [int(x) for x in ref[:, 1]]
+    # empty stream: (nil, io.EOF) at once
+    chk = chunkers.NewChunker("fastcdc", io.BytesIO(b""), _opts(DEF))
+    assert chk.Next() == (None, chunkers.EOF)
+
+
+def test_chunker_rejects_like_go():
+    _lib.ensure_init()
+    with pytest.raises(_lib.CdcError):
+        chunkers.NewChunker("ultracdc", io.BytesIO(b"x"), _opts(DEF))
+    with pytest.raises(_lib.CdcError):
+        chunkers.NewChunker("fastcdc", io.BytesIO(b"x"), chunkers.ChunkerOpts(65536, 65536, 1 << 20))
+
+
+def test_repository_chunkify_mirror(oracle):
+    """snapshot/backup.go:631-666 routing through Repository.Chunker."""
+    _lib.ensure_init()
+    repo = repository.Repository(DefaultConfiguration())
+    gear = _placeholder()
+    for size in [0, 1, 65535, 65536, 65537, 3 << 20]:
+        data = random_bytes(size, 300 + size % 97)
+        lens = repository.chunkify_lengths(repo, size, io.BytesIO(data.tobytes()))
+        ref = oracle.chunk(data, gear, chunkify=True, **DEF)
+        assert lens == [int(x) for x in ref[:, 1]], size
+    # lower-cased algorithm name, like repository.go:288
+    repo2 = repository.Repository(Configuration("FastCDC", 2048, 8192, 65536))
+    data = random_bytes(1 << 20, 301)
+    lens = repository.chunkify_lengths(repo2, data.size, io.BytesIO(data.tobytes()))
+    assert lens == [int(x) for x in oracle.chunk(data, gear, min_size=2048, normal_size=8192, max_size=65536)[:, 1]]
+
+
+def test_c4_mixed_corpus_host_path(oracle):
+    """BASELINE configs[4] shape (subsampled): Zipf-sized files, chunkify routing:
+    < MinSize files are one chunk, the rest go through ChunkBuffers."""
+    _lib.ensure_init()
+    sizes = zipf_sizes(300, 300)
+    files = [random_bytes(int(s), 400 + i) for i, s in enumerate(sizes)]
+    big = [f for f in files if f.size >= DEF["min_size"]]
+    res = chunkers.ChunkBuffers(big, _opts(DEF))
+    gear = _placeholder()
+    for i, f in enumerate(big):
+        assert_same(res[i], oracle.chunk(f, gear, **DEF), f"file {i} ({f.size} B)")
