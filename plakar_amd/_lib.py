@@ -134,8 +134,13 @@ _init_key = None
 
 def ensure_init(gear=None, mask_s=0, mask_l=0, cut_convention=0, dev_mask=0):
     """cdc_init once per parameter set (the Gear table / masks are library-global,
-    like the package-level G of ext chunkers/fastcdc)."""
+    like the package-level G of ext chunkers/fastcdc).  Called with no
+    arguments it initialises with the defaults only if the library is not
+    initialised yet, and otherwise keeps the current parameters."""
     global _init_key
+    explicit = (gear is not None or mask_s or mask_l or cut_convention or dev_mask)
+    if not explicit and _init_key is not None:
+        return
     key = (None if gear is None else tuple(int(x) for x in gear), int(mask_s), int(mask_l),
            int(cut_convention), int(dev_mask))
     if key == _init_key:

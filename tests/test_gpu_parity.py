@@ -60,7 +60,7 @@ def _reset_debug():
     device.set_debug_mode(0)
     yield
     device.set_debug_mode(0)
-    _lib.ensure_init()
+    _lib.ensure_init(gear=_lib.default_gear())
 
 
 # ---------------------------------------------------------------- golden vectors
