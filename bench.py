@@ -203,6 +203,9 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    L.cdc_shutdown()
 
 
 if __name__ == "__main__":

@@ -197,6 +197,7 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     B.cap1 = pl.cap1;
     B.cap2 = pl.cap2;
     B.seg = pl.seg;
+    B.scan_lane = pl.scan_lane;
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
     uint32_t segs = 0, blks = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
@@ -212,7 +213,7 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         D.task_base = tasks;
         segs += D.nseg;
         blks += uint32_t((lens[i] + kIdxBlock - 1) / kIdxBlock);
-        tasks += uint32_t((lens[i] + kScanTaskBytes - 1) / kScanTaskBytes);
+        tasks += uint32_t((lens[i] + 64ull * pl.scan_lane - 1) / (64ull * pl.scan_lane));
     }
     const Workspace W = carve(ws, pl, ctx->d_gear);
     return launch_batch(B, P, W, stream);

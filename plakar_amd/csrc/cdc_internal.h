@@ -14,9 +14,7 @@ constexpr uint32_t kIdxShift = 16;      // candidate-index block = 64 KiB of inp
 constexpr uint64_t kIdxBlock = 1ull << kIdxShift;
 constexpr uint32_t kIdxCap = 32;        // u16 entries per index block (one 64-B line)
 constexpr uint32_t kMaxSegs = 16384;    // resolution segments per buffer
-constexpr uint32_t kScanLaneBytes = 4096;                    // bytes hashed+tested per scan lane
-constexpr uint64_t kScanTaskBytes = 64ull * kScanLaneBytes;  // one wave = one scan task
-constexpr uint32_t kScanWavesPerWG = 8;
+constexpr uint32_t kScanLaneBytes = 8192;  // max bytes hashed+tested per scan lane (multiple of 128)
 constexpr uint32_t kWalkWavesPerWG = 16;
 constexpr uint64_t kUndet = ~0ull;      // "next chunk start not decided by the bytes present"
 
@@ -46,6 +44,8 @@ struct Batch {
     uint32_t total_segs, total_blks, total_tasks;
     uint32_t cap1, cap2;     // per-segment node capacities (speculative / junction walks)
     uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
+    uint32_t scan_lane;      // bytes per scan lane; one wave (scan task) = 64 lanes
+    uint32_t pad0;
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];
 };
@@ -71,6 +71,7 @@ constexpr uint32_t kConvOvf = 0xFFFFFFFDu;   // junction walk exceeded cap2 node
 
 struct Plan {
     uint64_t seg;
+    uint32_t scan_lane;
     uint32_t cap1, cap2;
     uint32_t total_segs, total_blks, total_tasks;
     size_t off_blk_cnt, off_blk_ent, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_w2_cnt,

@@ -46,9 +46,20 @@ static constexpr uint32_t kNtCap = 4096;        // emit: non-trivial junctions p
 // Byte address of entry b for this lane = (b << 8) | ((lane & 31) << 3),
 // built from the packed data word by one v_perm_b32.
 // ---------------------------------------------------------------------------
+// NT threads fill the 32-copy table: thread t owns copy (t & 31) of entries
+// (t >> 5) + k * NT/32; all its global loads are issued before any store.
+template <int NT>
 __device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gear)
 {
-    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) tab[i] = gear[i >> 5];
+    static_assert(NT % 32 == 0 && NT >= 64, "block size");
+    constexpr int kPer = 256 * 32 / NT;
+    constexpr int kStep = NT / 32;
+    const uint32_t c = threadIdx.x & 31u, e0 = threadIdx.x >> 5;
+    uint64_t v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) v[i] = gear[e0 + i * kStep];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) tab[(e0 + i * kStep) * 32 + c] = v[i];
 }
 
 __device__ __forceinline__ uint64_t lds_gear(const char *tab, uint32_t addr)
@@ -115,7 +126,7 @@ __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: full-window MaskS candidates of every byte into the index.
+// Scan helpers: full-window MaskS candidates of every byte into the index.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void index_append(uint32_t *cnt, uint16_t *ent, uint64_t pos)
 {
@@ -154,56 +165,190 @@ __device__ __forceinline__ void scan_group(const uint4 &d, uint64_t &fp, uint64_
     }
 }
 
-__device__ __forceinline__ void load8(uint4 (&d)[8], uint64_t a, uint64_t ae)
+// Software-pipelined form of the inner loop: the 16 Gear values of a group
+// are gathered (ds_read_b64) one group ahead of the multiply-free rolling
+// chain that consumes them, so LDS latency is not exposed per byte.
+__device__ __forceinline__ void gather16(uint64_t (&g)[16], const uint4 &d, const char *tab,
+                                         uint32_t laneoff)
 {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint64_t ga = a + 16u * i;
-        d[i] = ga < ae ? *reinterpret_cast<const uint4 *>(ga) : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < 16; ++k) g[k] = lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+}
+
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t roll16g(const uint64_t (&g)[16], uint64_t &fp, uint32_t mlo,
+                                            uint32_t mhi)
+{
+    uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        fp = (fp << 1) + g[k];
+        const uint32_t k0 = key_of(fp, mlo, mhi);
+        fp = (fp << 1) + g[k + 1];
+        acc = umin3(acc, k0, key_of(fp, mlo, mhi));
+    }
+    return acc;
+}
+
+__device__ __forceinline__ void record16g(const uint64_t (&g)[16], uint64_t f, uint64_t pos0,
+                                          uint32_t mlo, uint32_t mhi, uint32_t *cnt, uint16_t *ent)
+{
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        f = (f << 1) + g[k];
+        if (key_of(f, mlo, mhi) == 0) index_append(cnt, ent, pos0 + k);
     }
 }
 
-__global__ __launch_bounds__(kScanWavesPerWG * 64) void k_scan(const Batch B, const DevParams P,
-                                                              const Workspace W)
+// One interior 64-byte stage (4 groups, all positions tested), gathers one group ahead.
+__device__ __forceinline__ void fast_stage(const uint4 (&d)[4], uint64_t &fp, uint64_t pos0,
+                                           const char *tab, uint32_t laneoff, uint32_t mlo,
+                                           uint32_t mhi, uint32_t *cnt, uint16_t *ent)
 {
-    __shared__ uint64_t s_tab[256 * 32];
-    fill_gear_lds(s_tab, W.gear);
+    uint64_t ga[16], gb[16];
+    gather16(ga, d[0], tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    gather16(gb, d[1], tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    uint64_t f0 = fp;
+    if (roll16g(ga, fp, mlo, mhi) == 0) [[unlikely]] record16g(ga, f0, pos0, mlo, mhi, cnt, ent);
+    __builtin_amdgcn_sched_barrier(0);
+    gather16(ga, d[2], tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    f0 = fp;
+    if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 16, mlo, mhi, cnt, ent);
+    __builtin_amdgcn_sched_barrier(0);
+    gather16(gb, d[3], tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    f0 = fp;
+    if (roll16g(ga, fp, mlo, mhi) == 0) [[unlikely]] record16g(ga, f0, pos0 + 32, mlo, mhi, cnt, ent);
+    __builtin_amdgcn_sched_barrier(0);
+    f0 = fp;
+    if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 48, mlo, mhi, cnt, ent);
+}
+
+// ---------------------------------------------------------------------------
+// k_scan2: the same scan with coalesced LDS-DMA staging.  Each wave owns 64
+// lane segments; per 64-byte stage it issues 4 global_load_lds_dwordx4
+// (1 KiB each, every 64-B half line read whole by 4 adjacent lanes) into a
+// private 3-deep LDS ring, and each lane reads its own 64 bytes back with
+// ds_read_b128 through an XOR swizzle (piece k of segment s at slot
+// k ^ ((s >> 2) & 3)) that makes the reads bank-conflict-free.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kS2Waves = 8;
+constexpr uint32_t kS2Stage = 64;                     // bytes per lane per stage
+constexpr uint32_t kS2NBuf = 3;                       // ring depth (2 stages in flight)
+constexpr uint32_t kS2StageBytes = 64u * kS2Stage;    // per wave per stage
+constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
+
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
+{
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+__global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const DevParams P,
+                                                        const Workspace W)
+{
+    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kS2NBuf * kS2StageBytes];
+    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear);
     __syncthreads();
-    const char *tab = reinterpret_cast<const char *>(s_tab);
+    const char *tab = s_lds;
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
-    const uint32_t task = blockIdx.x * kScanWavesPerWG + (threadIdx.x >> 6);
+    const uint32_t task = blockIdx.x * kS2Waves + wave;
     if (task >= B.total_tasks) return;
     uint32_t b = 0;
     while (b + 1 < B.nbufs && task >= B.b[b + 1].task_base) ++b;
     const BufDesc &D = B.b[b];
 
-    const uint64_t s = uint64_t(task - D.task_base) * kScanTaskBytes + uint64_t(lane) * kScanLaneBytes;
-    if (s >= D.len) return;
-    const uint64_t e = min(s + kScanLaneBytes, D.len);
+    const uint64_t sl = B.scan_lane;                  // multiple of 128
     const uint64_t ub = reinterpret_cast<uint64_t>(D.data);
+    const uint64_t a0 = ub & ~15ull;                  // 16-aligned base
+    const uint64_t lo_ok = a0, hi_ok = (ub + D.len + 15) & ~15ull;  // safe (16-B blocks of the buffer)
+    const uint64_t seg0 = uint64_t(task - D.task_base) * 64u;       // first lane segment of the task
+    // this lane's tested range
+    const uint64_t s = (seg0 + lane) * sl;
+    const bool active = s < D.len;
+    const uint64_t e = active ? min(s + sl, D.len) : s;
     const uint64_t as = ub + s, ae = ub + e;
-    uint64_t a = (ub + (s >= kWarm ? s - kWarm : 0)) & ~15ull;
+    // stage t of segment q covers [S(q) + 64 t, +64), S(q) = align16(ub + q*sl) - 64
+    const uint32_t T = uint32_t((sl + 64u + (ub & 15u) + 63u) / 64u);
+    // the 4 segments whose pieces this lane loads: q_j = seg0 + 16 j + lane / 4
+    uint64_t src[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t q = seg0 + 16u * j + (lane >> 2);
+        const uint32_t k = (lane & 3u) ^ uint32_t((q >> 2) & 3u);
+        src[j] = ((ub + q * sl) & ~15ull) - 64u + 16u * k;
+    }
+    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes +
+                          wave * kS2NBuf * kS2StageBytes;
+    auto issue = [&](uint32_t t) {
+        const uint32_t dst = ring + (t % kS2NBuf) * kS2StageBytes;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t g = src[j] + 64ull * t;
+            if (g < lo_ok || g >= hi_ok) g = lo_ok;   // warm-up before byte 0 / past the end: ignored bytes
+            glds16(reinterpret_cast<const void *>(g), dst + 1024u * j);
+        }
+    };
     uint32_t *cnt = W.blk_cnt + D.blk_base;
     uint16_t *ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
     const uint32_t mlo = P.ms_lo, mhi = P.ms_hi;
+    const uint64_t S = ((ub + s) & ~15ull) - 64u;
+    const uint32_t swz = (lane >> 2) & 3u;
 
     uint64_t fp = 0;
-    uint4 x[8], y[8];
-    load8(x, a, ae);
-    // double-buffered 128-byte batches per lane: load batch i+1, roll batch i
-    while (a < ae) {
-        load8(y, a + 128, ae);
+    issue(0);
+    if (T > 1) issue(1);
+    for (uint32_t t = 0; t < T; ++t) {
+        if (t + 2 < T) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot being refilled are done
+            issue(t + 2);
+            wait_vmcnt<8>();
+        } else if (t + 1 < T) {
+            wait_vmcnt<4>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        if (active) {
+            const char *buf = s_lds + kGearLdsBytes + (wave * kS2NBuf + t % kS2NBuf) * kS2StageBytes + lane * 64u;
+            uint4 d[4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            scan_group(x[i], fp, a + 16u * i, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
-        a += 128;
-        if (a >= ae) break;
-        load8(x, a + 128, ae);
+            for (int g = 0; g < 4; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+            const uint64_t st0 = S + 64ull * t;
+            if (st0 >= as && st0 + 64 <= ae) {
+                fast_stage(d, fp, st0 - ub, tab, laneoff, mlo, mhi, cnt, ent);
+            } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            scan_group(y[i], fp, a + 16u * i, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
-        a += 128;
+                for (int g = 0; g < 4; ++g)
+                    scan_group(d[g], fp, st0 + 16u * g, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
+            }
+        }
     }
 }
 
@@ -394,7 +539,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, c
                                                                const Workspace W)
 {
     __shared__ uint64_t s_tab[256 * 32];
-    fill_gear_lds(s_tab, W.gear);
+    fill_gear_lds<kWalkWavesPerWG * 64>(s_tab, W.gear);
     __syncthreads();
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     if (g >= B.total_segs) return;
@@ -426,7 +571,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
                                                                const Workspace W)
 {
     __shared__ uint64_t s_tab[256 * 32];
-    fill_gear_lds(s_tab, W.gear);
+    fill_gear_lds<kWalkWavesPerWG * 64>(s_tab, W.gear);
     __syncthreads();
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     if (g >= B.total_segs) return;
@@ -507,6 +652,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum
 __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
 {
     __shared__ uint32_t s_nt[kNtCap];
+    __shared__ uint32_t s_ntc[kNtCap];  // w2_conv of each listed junction
     __shared__ uint32_t s_ivs[kNtCap], s_ive[kNtCap];
     __shared__ uint32_t s_wsum[16];
     __shared__ uint32_t s_m, s_niv, s_fail;
@@ -543,14 +689,18 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
         for (uint32_t base = 1; base < NS; base += blockDim.x) {
             const uint32_t q = base + tid;
             bool nt = false;
+            uint32_t c = 0;
             if (q < NS) {
-                const uint32_t c = W.w2_conv[G0 + q];
+                c = W.w2_conv[G0 + q];
                 nt = c >= kConvOvf || c != q;  // jump = c + 1 differs from q + 1
             }
             uint32_t tot;
             const uint32_t pre = block_excl_scan(nt ? 1u : 0u, s_wsum, tot);
             const uint32_t m0 = s_m;
-            if (nt && m0 + pre < kNtCap) s_nt[m0 + pre] = q;
+            if (nt && m0 + pre < kNtCap) {
+                s_nt[m0 + pre] = q;
+                s_ntc[m0 + pre] = c;
+            }
             __syncthreads();
             if (tid == 0) s_m = m0 + tot;
             __syncthreads();
@@ -566,7 +716,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
             for (uint32_t i = 0; i < m; ++i) {
                 const uint32_t p = s_nt[i];
                 if (p < cur) continue;  // skipped by an earlier junction walk
-                const uint32_t c = W.w2_conv[G0 + p];
+                const uint32_t c = s_ntc[i];
                 if (c == kConvOvf) {
                     fail = 1;
                     break;
@@ -685,7 +835,7 @@ __global__ __launch_bounds__(64) void k_fallback(const Batch B, const DevParams 
     const uint32_t b = blockIdx.x;
     if (W.flags[b] == 0) return;
     __shared__ uint64_t s_tab[256 * 32];
-    fill_gear_lds(s_tab, W.gear);
+    fill_gear_lds<64>(s_tab, W.gear);
     __syncthreads();
     const BufDesc &D = B.b[b];
     const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
@@ -731,13 +881,35 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     if (seg < need) seg = need;
     seg = (seg + 15) & ~15ull;
     plan->seg = seg;
+    // Scan lane length: enough lanes to give every CU one workgroup of 8 waves
+    // (one scan workgroup fills a CU's LDS), at most 8 KiB per lane.
+    uint64_t total = 0;
+    for (int i = 0; i < nbufs; ++i) total += lens[i];
+    static const uint64_t cus = [] {
+        int n = 0, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return uint64_t(n);
+    }();
+    uint64_t want = (total + cus * kS2Waves * 64 - 1) / (cus * kS2Waves * 64);
+    want = (want + 127) & ~127ull;
+    if (want < 512) want = 512;
+    if (want > kScanLaneBytes) want = kScanLaneBytes;
+    uint32_t lane = uint32_t(want);
+    if (const char *env = getenv("CDC_SCAN_LANE_BYTES")) {
+        const long v = atol(env);
+        if (v >= 256 && v <= (1 << 20) && v % 128 == 0) lane = uint32_t(v);
+    }
+    plan->scan_lane = lane;
+    const uint64_t task_bytes = 64ull * lane;
     plan->cap1 = uint32_t(seg / P.min_size + 3);
     plan->cap2 = 4 * plan->cap1 + 16;
     uint64_t segs = 0, blks = 0, tasks = 0;
     for (int i = 0; i < nbufs; ++i) {
         segs += (lens[i] + seg - 1) / seg;
         blks += (lens[i] + kIdxBlock - 1) / kIdxBlock;
-        tasks += (lens[i] + kScanTaskBytes - 1) / kScanTaskBytes;
+        tasks += (lens[i] + task_bytes - 1) / task_bytes;
     }
     if (segs >= 0xFFFF0000ull || blks >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
     plan->total_segs = uint32_t(segs);
@@ -801,8 +973,8 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         return CDC_E_DEVICE;
     if (prof) (void)hipEventRecord(pr.e0, st);
     if (B.total_tasks > 0)
-        hipLaunchKernelGGL(k_scan, dim3((B.total_tasks + kScanWavesPerWG - 1) / kScanWavesPerWG),
-                           dim3(kScanWavesPerWG * 64), 0, st, B, P, W);
+        hipLaunchKernelGGL(k_scan2, dim3((B.total_tasks + kS2Waves - 1) / kS2Waves),
+                           dim3(kS2Waves * 64), 0, st, B, P, W);
     if (prof) (void)hipEventRecord(pr.e1, st);
     if (B.total_segs > 0 && !B.force_fallback) {
         const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
