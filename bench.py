@@ -36,14 +36,37 @@ WORKLOADS = {
                nbuf=32, size=64 << 20, kind="random"),
     "c3": dict(desc="C3: 1x 1 GiB zeros + 1% random bytes per GPU (BASELINE configs[3], one GPU's share)",
                nbuf=1, size=1 << 30, kind="low_entropy"),
+    "c4": dict(desc="C4: Zipf(1.1) corpus of 4 KiB-128 MiB files, 512 per GPU (BASELINE configs[4], one GPU's "
+                    "share), host buffers in -> cut lists in host memory (PCIe-inclusive)",
+               nbuf=512, size=0, kind="zipf", host=True),
 }
 
 
-def make_buffers(torch, wl, rank, dev, size):
+def buffer_seeds(wl, rank, world):
+    """Seeds of the buffers rank `rank` chunks.  Work per GPU is fixed (weak
+    scaling): rank r owns buffers r*nbuf .. r*nbuf + nbuf - 1 of the global
+    workload, so at N GPUs the job covers N*nbuf independent buffers (C2 at
+    N = 8: the 256 x 64 MiB of BASELINE configs[2]).  No buffer is shared:
+    independent files shard one-per-GPU with no collective."""
+    assert 0 <= rank < world
+    return [1 + rank * wl["nbuf"] + i for i in range(wl["nbuf"])]
+
+
+def reduce_max(dist, world, value, dev):
+    """Max over ranks of a host float (the slowest rank sets the job time)."""
+    if world == 1:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_buffers(torch, wl, rank, dev, size, world=1):
     g = torch.Generator(device=dev)
     bufs = []
-    for i in range(wl["nbuf"]):
-        g.manual_seed(1 + 1000 * rank + i)
+    for seed in buffer_seeds(wl, rank, world):
+        g.manual_seed(seed)
         if wl["kind"] == "random":
             t = torch.randint(0, 256, (size,), dtype=torch.uint8, device=dev, generator=g)
         else:
@@ -53,6 +76,39 @@ def make_buffers(torch, wl, rank, dev, size):
             t[pos] = torch.randint(0, 256, (k,), dtype=torch.uint8, device=dev, generator=g)
         bufs.append(t)
     return bufs
+
+
+def zipf_sizes(count, seed, s=1.1, unit=4096, kmax=32768):
+    """C4 file sizes: bounded Zipf(s) over {unit * k, k = 1..kmax}."""
+    import numpy as np
+    k = np.arange(1, kmax + 1, dtype=np.float64)
+    p = k ** -s
+    cdf = np.cumsum(p) / p.sum()
+    u = (np.random.PCG64(seed).random_raw(count) >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    return ((np.searchsorted(cdf, u) + 1) * unit).astype(np.int64)
+
+
+def make_host_corpus(wl, rank, world):
+    """C4: the rank's share of the corpus as pageable host buffers (uniform bytes)."""
+    import numpy as np
+    sizes = zipf_sizes(wl["nbuf"] * world, 300)[rank * wl["nbuf"]:(rank + 1) * wl["nbuf"]]
+    out = []
+    for seed, n in zip(buffer_seeds(wl, rank, world), sizes):
+        n = int(n)
+        out.append(np.random.PCG64(seed).random_raw((n + 7) // 8).view(np.uint8)[:n].copy())
+    return out
+
+
+def e2e_host_rate(chunkers, opts, host_bufs, reps):
+    """PCIe-inclusive rate of the host-buffer path (cdc_chunk: pageable host
+    bytes -> pinned staging -> HBM -> kernels -> cut lists in host memory)."""
+    chunkers.ChunkBuffers(host_bufs, opts)  # warm-up: arenas, pinned staging
+    total = sum(a.size for a in host_bufs)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = chunkers.ChunkBuffers(host_bufs, opts)
+    el = time.perf_counter() - t0
+    return total * reps / el / GIB, el / reps, res
 
 
 def load_traffic(workload):
@@ -84,7 +140,8 @@ def cpu_baseline(bufs_host, cuts_dev, opts, seconds):
         for i, a in enumerate(bufs_host):
             ref = orc.chunk(a, gear, **kw)
             if reps == 0:
-                got = cuts_dev[i].cpu().numpy().astype(np.uint64)
+                got = cuts_dev[i]
+                got = np.asarray(got.cpu().numpy() if hasattr(got, "cpu") else got).astype(np.uint64)
                 parity &= bool(got.shape == ref.shape and (got == ref).all())
             done_bytes += a.size
         reps += 1
@@ -106,6 +163,8 @@ def main():
     ap.add_argument("--size-mib", type=int, default=0, help="override the per-buffer size (debug)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-reps", type=int, default=3,
+                    help="reps of the PCIe-inclusive host-buffer leg (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -130,15 +189,34 @@ def main():
             dist.barrier()
 
     wl = WORKLOADS[args.workload]
-    size = (args.size_mib << 20) if args.size_mib else wl["size"]
+    host_mode = wl.get("host", False)
     opts = chunkers.ChunkerOpts(MinSize=64 * 1024, NormalSize=1 << 20, MaxSize=4 << 20)
-    _lib.ensure_init(dev_mask=0)
-    bufs = make_buffers(torch, wl, rank, dev, size)
-    batch = device.DeviceBatch(bufs, opts, final=True, device=local)
+    _lib.ensure_init(dev_mask=1 << local)  # this rank's GPU only
     L = _lib.lib()
 
+    routed_bytes = 0
+    if host_mode:
+        corpus = make_host_corpus(wl, rank, world)
+        # plakar chunkify routing (snapshot/backup.go:631-644): files < MinSize are one chunk, no CDC
+        host_bufs = [a for a in corpus if a.size >= opts.MinSize]
+        routed_bytes = sum(a.size for a in corpus if a.size < opts.MinSize)
+        per_rank_bytes = sum(a.size for a in host_bufs)
+        nbufs = len(host_bufs)
+
+        def step():
+            return chunkers.ChunkBuffers(host_bufs, opts)
+    else:
+        size = (args.size_mib << 20) if args.size_mib else wl["size"]
+        bufs = make_buffers(torch, wl, rank, dev, size, world)
+        batch = device.DeviceBatch(bufs, opts, final=True, device=local)
+        per_rank_bytes = sum(t.numel() for t in bufs)
+        nbufs = len(bufs)
+
+        def step():
+            batch.launch()
+
     for _ in range(args.warmup):
-        batch.launch()
+        step()
     torch.cuda.synchronize(dev)
     barrier()
     L.cdc_profile_collect(None, None, None, None)
@@ -147,7 +225,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        batch.launch()
+        out = step()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
@@ -156,49 +234,76 @@ def main():
     launches, scan_bytes = ctypes.c_uint64(), ctypes.c_uint64()
     _lib.check(L.cdc_profile_collect(ctypes.byref(scan_ms), ctypes.byref(pipe_ms),
                                      ctypes.byref(launches), ctypes.byref(scan_bytes)), "profile")
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    cuts, res = batch.results()
-    nchunks = int(res[:, 0].sum())
-    per_rank_bytes = sum(t.numel() for t in bufs)
+    elapsed = reduce_max(dist, world, t1 - t0, dev)
     value = world * per_rank_bytes * args.steps / elapsed / GIB
+
+    if host_mode:
+        host_cuts = out
+        nchunks = sum(len(c) for c in host_cuts)
+    else:
+        cuts, res = batch.results()
+        nchunks = int(res[:, 0].sum())
 
     n = max(int(launches.value), 1)
     scan_avg_ms = scan_ms.value / n
     pipe_avg_ms = pipe_ms.value / n
     bytes_per_launch = scan_bytes.value / n
-    achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
+    achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=load_traffic(args.workload),
-                    kernel="k_scan", kernel_avg_ms=round(scan_avg_ms, 4),
+                    kernel="k_scan2", kernel_avg_ms=round(scan_avg_ms, 4),
                     algorithmic_bytes_per_launch=int(bytes_per_launch),
+                    launches_per_step=round(n / max(args.steps, 1), 2),
                     pipeline_avg_ms=round(pipe_avg_ms, 4))
 
-    baseline, parity = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        host = [t.cpu().numpy() for t in bufs[:1]]
-        baseline, parity = cpu_baseline(host, cuts[:1], opts, args.cpu_seconds)
+    baseline, parity, e2e = None, None, None
+    if rank == 0 and world == 1:
+        import numpy as np
+        if host_mode:
+            sample, tot = [], 0
+            for a in host_bufs:  # bounded sample: the first ~1 GiB of the corpus
+                if tot >= (1 << 30):
+                    break
+                sample.append(a)
+                tot += a.size
+            sample_cuts = [np.asarray(c) for c in host_cuts[:len(sample)]]
+        else:
+            host = [t.cpu().numpy() for t in bufs[:1]]
+            if args.e2e_reps > 0:
+                rate, sec, e2e_cuts = e2e_host_rate(chunkers, opts, host, args.e2e_reps)
+                dev_cuts = [c.cpu().numpy().astype(np.uint64) for c in cuts[:len(e2e_cuts)]]
+                same = all(a.shape == d.shape and bool((a == d).all()) for a, d in zip(e2e_cuts, dev_cuts))
+                e2e = dict(value=round(rate, 2), unit="GiB/s", ms_per_call=round(sec * 1e3, 2),
+                           path="cdc_chunk: pageable host -> pinned bounce -> H2D -> kernels -> D2H cut lists",
+                           sample=f"{len(host)} x {host[0].size / GIB:.3g} GiB, {args.e2e_reps} reps",
+                           same_cuts_as_device_path=same)
+            sample = host
+            sample_cuts = cuts[:1]
+        if not args.no_cpu_baseline:
+            baseline, parity = cpu_baseline(sample, sample_cuts, opts, args.cpu_seconds)
 
     if rank == 0:
+        config = {"workload": wl["desc"], "bytes_per_gpu": per_rank_bytes,
+                  "global_bytes": per_rank_bytes * world, "buffers_per_gpu": nbufs,
+                  "chunk_params": "FASTCDC min 65536 / normal 1048576 / max 4194304",
+                  "gear": "placeholder (v0.0.8 table unavailable; see DESIGN.md)",
+                  "parallelism": f"independent buffers, 1 rank per GPU x {world}, no collective",
+                  "chunks_per_step": nchunks}
+        if host_mode:
+            config["routed_bytes_per_gpu"] = routed_bytes
+            config["timing"] = "end-to-end incl. host->device copies and cut lists back to host"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (torch Philox uniform bytes generated on the GPU; no dataset)",
-            "config": {"workload": wl["desc"], "bytes_per_gpu": per_rank_bytes,
-                       "global_bytes": per_rank_bytes * world, "buffers_per_gpu": len(bufs),
-                       "chunk_params": "FASTCDC min 65536 / normal 1048576 / max 4194304",
-                       "gear": "placeholder (v0.0.8 table unavailable; see DESIGN.md)",
-                       "parallelism": f"independent buffers, 1 rank per GPU x {world}, no collective",
-                       "chunks_per_step": nchunks},
+            "data": ("synthetic (numpy PCG64 uniform bytes in host memory; no dataset)" if host_mode else
+                     "synthetic (torch Philox uniform bytes generated on the GPU; no dataset)"),
+            "config": config,
             "roofline": roofline,
             "cpu_baseline": baseline,
             "parity_vs_oracle": parity,
+            "e2e_host_path": e2e,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -26,13 +26,9 @@ namespace {
 constexpr uint64_t kDefaultMaskS = 0x0003590703530000ull;  // FastCDC paper MaskS (15 bits)
 constexpr uint64_t kDefaultMaskL = 0x0000d90003530000ull;  // FastCDC paper MaskL (11 bits)
 
-struct DeviceCtx {
-    int device = -1;
-    uint64_t *d_gear = nullptr;
-    hipStream_t stream = nullptr;
-    std::mutex mu;
-    // host-buffer path arenas (grown on demand)
-    uint8_t *h_stage = nullptr;
+// One in-flight launch group of the host-buffer path: device input, workspace,
+// cut lists and results, plus the event that marks its results as copied back.
+struct Slot {
     uint8_t *d_in = nullptr;
     uint64_t in_cap = 0;
     void *d_ws = nullptr;
@@ -42,6 +38,23 @@ struct DeviceCtx {
     uint64_t cuts_cap = 0;
     cdc_result *d_res = nullptr;
     cdc_result *h_res = nullptr;
+    hipEvent_t staged = nullptr;  // copy stream: input bytes are on the device
+    hipEvent_t done = nullptr;    // compute stream: results are in h_res / h_cuts
+};
+
+constexpr int kBounces = 2;
+
+struct DeviceCtx {
+    int device = -1;
+    uint64_t *d_gear = nullptr;
+    hipStream_t stream = nullptr;  // kernels + result copies
+    hipStream_t copy = nullptr;    // host -> device input copies
+    std::mutex mu;
+    Slot slot[2];
+    uint8_t *bounce[kBounces] = {nullptr, nullptr};  // pinned staging for H2D
+    uint64_t bounce_cap = 0;
+    hipEvent_t bounce_ev[kBounces] = {nullptr, nullptr};
+    int next_bounce = 0;
 };
 
 struct Global {
@@ -107,56 +120,83 @@ DevParams make_params(const cdc_opts *o)
         if ((x) != hipSuccess) return CDC_E_DEVICE; \
     } while (0)
 
-void free_ctx_buffers(DeviceCtx *c)
+void free_slot(Slot &sl)
 {
-    if (c->h_stage) (void)hipHostFree(c->h_stage);
-    if (c->d_in) (void)hipFree(c->d_in);
-    if (c->d_ws) (void)hipFree(c->d_ws);
-    if (c->d_cuts) (void)hipFree(c->d_cuts);
-    if (c->h_cuts) (void)hipHostFree(c->h_cuts);
-    if (c->d_res) (void)hipFree(c->d_res);
-    if (c->h_res) (void)hipHostFree(c->h_res);
-    c->h_stage = c->d_in = nullptr;
-    c->d_ws = nullptr;
-    c->d_cuts = c->h_cuts = nullptr;
-    c->d_res = c->h_res = nullptr;
-    c->in_cap = c->ws_cap = c->cuts_cap = 0;
+    if (sl.d_in) (void)hipFree(sl.d_in);
+    if (sl.d_ws) (void)hipFree(sl.d_ws);
+    if (sl.d_cuts) (void)hipFree(sl.d_cuts);
+    if (sl.h_cuts) (void)hipHostFree(sl.h_cuts);
+    if (sl.d_res) (void)hipFree(sl.d_res);
+    if (sl.h_res) (void)hipHostFree(sl.h_res);
+    if (sl.staged) (void)hipEventDestroy(sl.staged);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+    sl = Slot();
 }
 
-int grow(DeviceCtx *c, uint64_t in_bytes, uint64_t ws_bytes, uint64_t ncuts)
+void free_ctx_buffers(DeviceCtx *c)
 {
-    if (in_bytes > c->in_cap) {
-        if (c->h_stage) (void)hipHostFree(c->h_stage);
-        if (c->d_in) (void)hipFree(c->d_in);
-        c->h_stage = nullptr;
-        c->d_in = nullptr;
-        c->in_cap = 0;
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), in_bytes, hipHostMallocDefault));
-        HIPCHK(hipMalloc(reinterpret_cast<void **>(&c->d_in), in_bytes));
-        c->in_cap = in_bytes;
+    for (auto &sl : c->slot) free_slot(sl);
+    for (int k = 0; k < kBounces; ++k) {
+        if (c->bounce[k]) (void)hipHostFree(c->bounce[k]);
+        if (c->bounce_ev[k]) (void)hipEventDestroy(c->bounce_ev[k]);
+        c->bounce[k] = nullptr;
+        c->bounce_ev[k] = nullptr;
     }
-    if (ws_bytes > c->ws_cap) {
-        if (c->d_ws) (void)hipFree(c->d_ws);
-        c->d_ws = nullptr;
-        c->ws_cap = 0;
-        HIPCHK(hipMalloc(&c->d_ws, ws_bytes));
-        c->ws_cap = ws_bytes;
+    c->bounce_cap = 0;
+}
+
+// Grow a slot's buffers; the slot must be idle (its last group harvested).
+int grow_slot(Slot &sl, uint64_t in_bytes, uint64_t ws_bytes, uint64_t ncuts)
+{
+    if (!sl.staged) HIPCHK(hipEventCreateWithFlags(&sl.staged, hipEventDisableTiming));
+    if (!sl.done) HIPCHK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    if (in_bytes > sl.in_cap) {
+        if (sl.d_in) (void)hipFree(sl.d_in);
+        sl.d_in = nullptr;
+        sl.in_cap = 0;
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&sl.d_in), in_bytes));
+        sl.in_cap = in_bytes;
     }
-    if (ncuts > c->cuts_cap) {
-        if (c->d_cuts) (void)hipFree(c->d_cuts);
-        if (c->h_cuts) (void)hipHostFree(c->h_cuts);
-        c->d_cuts = c->h_cuts = nullptr;
-        c->cuts_cap = 0;
-        HIPCHK(hipMalloc(reinterpret_cast<void **>(&c->d_cuts), ncuts * sizeof(cdc_cut)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_cuts), ncuts * sizeof(cdc_cut),
+    if (ws_bytes > sl.ws_cap) {
+        if (sl.d_ws) (void)hipFree(sl.d_ws);
+        sl.d_ws = nullptr;
+        sl.ws_cap = 0;
+        HIPCHK(hipMalloc(&sl.d_ws, ws_bytes));
+        sl.ws_cap = ws_bytes;
+    }
+    if (ncuts > sl.cuts_cap) {
+        if (sl.d_cuts) (void)hipFree(sl.d_cuts);
+        if (sl.h_cuts) (void)hipHostFree(sl.h_cuts);
+        sl.d_cuts = sl.h_cuts = nullptr;
+        sl.cuts_cap = 0;
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&sl.d_cuts), ncuts * sizeof(cdc_cut)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sl.h_cuts), ncuts * sizeof(cdc_cut),
                              hipHostMallocDefault));
-        c->cuts_cap = ncuts;
+        sl.cuts_cap = ncuts;
     }
-    if (!c->d_res) {
-        HIPCHK(hipMalloc(reinterpret_cast<void **>(&c->d_res), kMaxBufsPerLaunch * sizeof(cdc_result)));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->h_res),
+    if (!sl.d_res) {
+        HIPCHK(hipMalloc(reinterpret_cast<void **>(&sl.d_res), kMaxBufsPerLaunch * sizeof(cdc_result)));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&sl.h_res),
                              kMaxBufsPerLaunch * sizeof(cdc_result), hipHostMallocDefault));
     }
+    return CDC_OK;
+}
+
+int grow_bounce(DeviceCtx *c, uint64_t bytes)
+{
+    if (bytes <= c->bounce_cap) return CDC_OK;
+    HIPCHK(hipStreamSynchronize(c->copy));
+    for (int k = 0; k < kBounces; ++k) {
+        if (c->bounce[k]) (void)hipHostFree(c->bounce[k]);
+        c->bounce[k] = nullptr;
+    }
+    c->bounce_cap = 0;
+    for (int k = 0; k < kBounces; ++k) {
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&c->bounce[k]), bytes, hipHostMallocDefault));
+        if (!c->bounce_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->bounce_ev[k], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->bounce_ev[k], c->copy));
+    }
+    c->bounce_cap = bytes;
     return CDC_OK;
 }
 
@@ -198,6 +238,11 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     B.cap2 = pl.cap2;
     B.seg = pl.seg;
     B.scan_lane = pl.scan_lane;
+    static const uint32_t dbg = [] {
+        const char *e = getenv("CDC_DEBUG_PHASE");
+        return e ? uint32_t(atoi(e)) : 0u;
+    }();
+    B.debug = dbg;
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
     uint32_t segs = 0, blks = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
@@ -251,117 +296,200 @@ struct HostJob {
 
 uint64_t max_cuts_for(uint64_t len, uint32_t min_size) { return len / min_size + 2; }
 
-// Process host jobs on one device: pack whole buffers into the arena; buffers
-// larger than the arena are chunked as streams of arena-sized windows.
+uint64_t env_mb(const char *name, uint64_t def_mb, uint64_t min_mb)
+{
+    if (const char *e = getenv(name)) {
+        const long v = atol(e);
+        if (v >= long(min_mb)) return uint64_t(v) << 20;
+    }
+    return def_mb << 20;
+}
+
+// Pageable -> pinned copy, split over a few host threads: one thread's
+// memcpy (~10 GB/s) would otherwise cap the PCIe-inclusive rate.
+constexpr int kCopyThreads = 4;
+
+void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t len)
+{
+    constexpr uint64_t kMinPiece = 4ull << 20;
+    const int nt = int(std::min<uint64_t>(kCopyThreads, (len + kMinPiece - 1) / kMinPiece));
+    if (nt <= 1) {
+        std::memcpy(dst, src, len);
+        return;
+    }
+    const uint64_t per = ((len + nt - 1) / nt + 4095) & ~4095ull;
+    std::thread th[kCopyThreads];
+    for (int t = 1; t < nt; ++t) {
+        const uint64_t o = per * t;
+        if (o >= len) break;
+        th[t] = std::thread([=] { std::memcpy(dst + o, src + o, std::min(per, len - o)); });
+    }
+    std::memcpy(dst, src, std::min(per, len));
+    for (int t = 1; t < nt; ++t)
+        if (th[t].joinable()) th[t].join();
+}
+
+// Copy len host bytes to d_dst through the pinned bounce buffers on the copy
+// stream.  Returns once the last piece is queued; the host fills bounce k+1
+// while the copy engine drains bounce k.
+int stage(DeviceCtx *c, uint8_t *d_dst, const uint8_t *src, uint64_t len)
+{
+    uint64_t off = 0;
+    while (off < len) {
+        const int k = c->next_bounce;
+        c->next_bounce = (k + 1) % kBounces;
+        HIPCHK(hipEventSynchronize(c->bounce_ev[k]));
+        const uint64_t n = std::min(c->bounce_cap, len - off);
+        par_memcpy(c->bounce[k], src + off, n);
+        HIPCHK(hipMemcpyAsync(d_dst + off, c->bounce[k], n, hipMemcpyHostToDevice, c->copy));
+        HIPCHK(hipEventRecord(c->bounce_ev[k], c->copy));
+        off += n;
+    }
+    return CDC_OK;
+}
+
+struct Pending {
+    bool active = false;
+    std::vector<HostJob *> jobs;
+    std::vector<uint64_t> cut_off;
+};
+
+// Chunk one buffer too large to hold on the device as a stream of windows
+// (final = 0 except the last; each window resumes at the previous one's
+// `consumed`).  Sequential: the next window's start depends on this one.
+int run_windowed(DeviceCtx *ctx, const DevParams &P, const cdc_opts *o, HostJob *job, uint64_t window)
+{
+    Slot &sl = ctx->slot[0];
+    const uint64_t ncap = max_cuts_for(window, o->min_size);
+    uint64_t off = 0;
+    while (off < job->len) {
+        const uint64_t w = std::min(window, job->len - off);
+        const int fin = off + w == job->len;
+        uint64_t need = 0;
+        int st = group_ws_bytes(&w, 1, P, &need);
+        if (st != CDC_OK) return st;
+        st = grow_slot(sl, window, need, ncap);
+        if (st != CDC_OK) return st;
+        st = stage(ctx, sl.d_in, job->data + off, w);
+        if (st != CDC_OK) return st;
+        HIPCHK(hipEventRecord(sl.staged, ctx->copy));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, sl.staged, 0));
+        const void *dp = sl.d_in;
+        cdc_cut *cp = sl.d_cuts;
+        const uint64_t cap = sl.cuts_cap;
+        cdc_result *rp = sl.d_res;
+        st = run_group(ctx, P, &dp, &w, 1, fin, &cp, &cap, &rp, sl.d_ws, sl.ws_cap, ctx->stream);
+        if (st != CDC_OK) return st;
+        HIPCHK(hipMemcpyAsync(sl.h_res, sl.d_res, sizeof(cdc_result), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        const cdc_result r = sl.h_res[0];
+        if (r.status != CDC_OK) return int(r.status);
+        if (r.ncuts) {
+            HIPCHK(hipMemcpyAsync(sl.h_cuts, sl.d_cuts, r.ncuts * sizeof(cdc_cut), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+        }
+        for (uint64_t k = 0; k < r.ncuts; ++k) {
+            cdc_cut c = sl.h_cuts[k];
+            c.offset += off;
+            job->cuts.push_back(c);
+        }
+        if (!fin && r.consumed == 0) return CDC_E_DEVICE;  // cannot happen: window >= 4 * Max
+        off += fin ? w : r.consumed;
+    }
+    return CDC_OK;
+}
+
+// Process host jobs on one device as a two-slot pipeline.  Buffers are packed
+// into launch groups (<= kMaxBufsPerLaunch buffers, <= CDC_HOST_GROUP_MB bytes;
+// one larger buffer forms a group of its own).  While the compute stream
+// chunks group g in slot g % 2, the host stages group g + 1 into the other
+// slot through the pinned bounce buffers on the copy stream.  Only a buffer
+// larger than CDC_HOST_MAXBUF_MB (default 16 GiB of the 288 GB of HBM) is
+// chunked as a stream of windows.
 int run_host_jobs(DeviceCtx *ctx, const cdc_opts *o, std::vector<HostJob *> &jobs)
 {
     std::lock_guard<std::mutex> lock(ctx->mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return CDC_E_DEVICE;
     const DevParams P = make_params(o);
-    uint64_t arena = 256ull << 20;
-    if (const char *env = getenv("CDC_HOST_ARENA_MB")) {
-        const long v = atol(env);
-        if (v >= 16) arena = uint64_t(v) << 20;
-    }
-    arena = std::max<uint64_t>(arena, 4ull * o->max_size + 4096);
-    const uint64_t ncap = arena / o->min_size + 2 * kMaxBufsPerLaunch + 2;
-    int st = grow(ctx, arena, 0, ncap);
+    const uint64_t budget = std::max<uint64_t>(env_mb("CDC_HOST_GROUP_MB", 1024, 16), 4ull * o->max_size + 4096);
+    const uint64_t maxbuf = std::max<uint64_t>(env_mb("CDC_HOST_MAXBUF_MB", 16384, 16), budget);
+    if (!ctx->copy) HIPCHK(hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking));
+    int st = grow_bounce(ctx, std::min<uint64_t>(64ull << 20, budget));
     if (st != CDC_OK) return st;
-    // the workspace is sized per launch group, right before the launch
-    auto ensure_ws = [&](const uint64_t *lens, int n) {
-        uint64_t need = 0;
-        const int r = group_ws_bytes(lens, n, P, &need);
-        return r != CDC_OK ? r : grow(ctx, arena, need, ncap);
+
+    Pending pend[2];
+    auto harvest = [&](int s) -> int {
+        Pending &pd = pend[s];
+        if (!pd.active) return CDC_OK;
+        pd.active = false;
+        Slot &sl = ctx->slot[s];
+        HIPCHK(hipEventSynchronize(sl.done));
+        for (size_t i = 0; i < pd.jobs.size(); ++i) {
+            const cdc_result r = sl.h_res[i];
+            if (r.status != CDC_OK) return int(r.status);
+            pd.jobs[i]->cuts.assign(sl.h_cuts + pd.cut_off[i], sl.h_cuts + pd.cut_off[i] + r.ncuts);
+        }
+        return CDC_OK;
     };
 
+    int cur = 0;
     size_t j = 0;
     while (j < jobs.size()) {
-        HostJob *job = jobs[j];
-        if (job->len > arena) {
-            // stream a large buffer through the arena
-            uint64_t off = 0;
-            while (off < job->len) {
-                const uint64_t w = std::min(arena, job->len - off);
-                const int fin = off + w == job->len;
-                std::memcpy(ctx->h_stage, job->data + off, w);
-                HIPCHK(hipMemcpyAsync(ctx->d_in, ctx->h_stage, w, hipMemcpyHostToDevice, ctx->stream));
-                const void *dp = ctx->d_in;
-                cdc_cut *cp = ctx->d_cuts;
-                const uint64_t cap = ctx->cuts_cap;
-                cdc_result *rp = ctx->d_res;
-                st = ensure_ws(&w, 1);
-                if (st != CDC_OK) return st;
-                st = run_group(ctx, P, &dp, &w, 1, fin, &cp, &cap, &rp, ctx->d_ws, ctx->ws_cap,
-                               ctx->stream);
-                if (st != CDC_OK) return st;
-                HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(cdc_result),
-                                      hipMemcpyDeviceToHost, ctx->stream));
-                HIPCHK(hipStreamSynchronize(ctx->stream));
-                const cdc_result r = ctx->h_res[0];
-                if (r.status != CDC_OK) return int(r.status);
-                if (r.ncuts)
-                    HIPCHK(hipMemcpy(ctx->h_cuts, ctx->d_cuts, r.ncuts * sizeof(cdc_cut),
-                                     hipMemcpyDeviceToHost));
-                for (uint64_t k = 0; k < r.ncuts; ++k) {
-                    cdc_cut c = ctx->h_cuts[k];
-                    c.offset += off;
-                    job->cuts.push_back(c);
-                }
-                if (!fin && r.consumed == 0) return CDC_E_DEVICE;  // no progress: cannot happen
-                off += fin ? w : r.consumed;
-            }
+        if (jobs[j]->len > maxbuf) {
+            if ((st = harvest(0)) != CDC_OK || (st = harvest(1)) != CDC_OK) return st;
+            st = run_windowed(ctx, P, o, jobs[j], budget);
+            if (st != CDC_OK) return st;
             ++j;
             continue;
         }
-        // pack as many whole buffers as fit
         std::vector<HostJob *> group;
-        std::vector<uint64_t> offs, lens;
-        uint64_t used = 0;
-        while (j < jobs.size() && group.size() < size_t(kMaxBufsPerLaunch) &&
-               jobs[j]->len <= arena && used + jobs[j]->len <= arena) {
-            group.push_back(jobs[j]);
+        std::vector<uint64_t> offs, lens, caps, cut_off;
+        uint64_t used = 0, ncuts = 0;
+        while (j < jobs.size() && group.size() < size_t(kMaxBufsPerLaunch) && jobs[j]->len <= maxbuf &&
+               (group.empty() || used + jobs[j]->len <= budget)) {
+            HostJob *jb = jobs[j++];
+            group.push_back(jb);
             offs.push_back(used);
-            lens.push_back(jobs[j]->len);
-            used = (used + jobs[j]->len + 255) & ~255ull;
-            ++j;
+            lens.push_back(jb->len);
+            caps.push_back(max_cuts_for(jb->len, o->min_size));
+            cut_off.push_back(ncuts);
+            ncuts += caps.back();
+            used = (used + jb->len + 255) & ~255ull;
         }
-        for (size_t i = 0; i < group.size(); ++i)
-            std::memcpy(ctx->h_stage + offs[i], group[i]->data, group[i]->len);
-        if (used) HIPCHK(hipMemcpyAsync(ctx->d_in, ctx->h_stage, std::min(used, arena),
-                                        hipMemcpyHostToDevice, ctx->stream));
+        const int s = cur;
+        cur ^= 1;
+        if ((st = harvest(s)) != CDC_OK) return st;  // the slot's previous group
+        Slot &sl = ctx->slot[s];
         const int n = int(group.size());
+        uint64_t need = 0;
+        if ((st = group_ws_bytes(lens.data(), n, P, &need)) != CDC_OK) return st;
+        if ((st = grow_slot(sl, used, need, ncuts)) != CDC_OK) return st;
+        for (int i = 0; i < n; ++i)
+            if ((st = stage(ctx, sl.d_in + offs[i], group[i]->data, lens[i])) != CDC_OK) return st;
+        HIPCHK(hipEventRecord(sl.staged, ctx->copy));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, sl.staged, 0));
         std::vector<const void *> dp(n);
         std::vector<cdc_cut *> cp(n);
-        std::vector<uint64_t> caps(n);
         std::vector<cdc_result *> rp(n);
-        uint64_t cut_off = 0;
         for (int i = 0; i < n; ++i) {
-            dp[i] = ctx->d_in + offs[i];
-            cp[i] = ctx->d_cuts + cut_off;
-            caps[i] = max_cuts_for(lens[i], o->min_size);
-            cut_off += caps[i];
-            rp[i] = ctx->d_res + i;
+            dp[i] = sl.d_in + offs[i];
+            cp[i] = sl.d_cuts + cut_off[i];
+            rp[i] = sl.d_res + i;
         }
-        st = ensure_ws(lens.data(), n);
+        st = run_group(ctx, P, dp.data(), lens.data(), n, 1, cp.data(), caps.data(), rp.data(), sl.d_ws,
+                       sl.ws_cap, ctx->stream);
         if (st != CDC_OK) return st;
-        st = run_group(ctx, P, dp.data(), lens.data(), n, 1, cp.data(), caps.data(), rp.data(),
-                       ctx->d_ws, ctx->ws_cap, ctx->stream);
-        if (st != CDC_OK) return st;
-        HIPCHK(hipMemcpyAsync(ctx->h_res, ctx->d_res, n * sizeof(cdc_result),
-                              hipMemcpyDeviceToHost, ctx->stream));
-        if (cut_off)
-            HIPCHK(hipMemcpyAsync(ctx->h_cuts, ctx->d_cuts, cut_off * sizeof(cdc_cut),
-                                  hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        cut_off = 0;
-        for (int i = 0; i < n; ++i) {
-            const cdc_result r = ctx->h_res[i];
-            if (r.status != CDC_OK) return int(r.status);
-            group[i]->cuts.assign(ctx->h_cuts + cut_off, ctx->h_cuts + cut_off + r.ncuts);
-            cut_off += caps[i];
-        }
+        HIPCHK(hipMemcpyAsync(sl.h_res, sl.d_res, n * sizeof(cdc_result), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(sl.h_cuts, sl.d_cuts, ncuts * sizeof(cdc_cut), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        HIPCHK(hipEventRecord(sl.done, ctx->stream));
+        pend[s].active = true;
+        pend[s].jobs = std::move(group);
+        pend[s].cut_off = std::move(cut_off);
     }
-    return CDC_OK;
+    if ((st = harvest(0)) != CDC_OK) return st;
+    return harvest(1);
 }
 
 }  // namespace
@@ -481,9 +609,11 @@ void cdc_shutdown(void)
     for (auto *c : g.devs) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
-        free_ctx_buffers(c);
         if (c->d_gear) (void)hipFree(c->d_gear);
+        if (c->copy) (void)hipStreamSynchronize(c->copy);
+        free_ctx_buffers(c);
         if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->copy) (void)hipStreamDestroy(c->copy);
         delete c;
     }
     g.devs.clear();

@@ -15,7 +15,7 @@ constexpr uint64_t kIdxBlock = 1ull << kIdxShift;
 constexpr uint32_t kIdxCap = 32;        // u16 entries per index block (one 64-B line)
 constexpr uint32_t kMaxSegs = 16384;    // resolution segments per buffer
 constexpr uint32_t kScanLaneBytes = 8192;  // max bytes hashed+tested per scan lane (multiple of 128)
-constexpr uint32_t kWalkWavesPerWG = 16;
+constexpr uint32_t kWalkWavesPerWG = 4;   // latency-bound walkers: registers over occupancy
 constexpr uint64_t kUndet = ~0ull;      // "next chunk start not decided by the bytes present"
 
 // Chunker parameters as the kernels use them.
@@ -45,7 +45,7 @@ struct Batch {
     uint32_t cap1, cap2;     // per-segment node capacities (speculative / junction walks)
     uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
     uint32_t scan_lane;      // bytes per scan lane; one wave (scan task) = 64 lanes
-    uint32_t pad0;
+    uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];
 };

@@ -6,8 +6,9 @@
 // layout and the roofline of each kernel.
 //
 // Pipeline per launch group (<= 32 independent buffers):
-//   k_scan      HBM-bound byte scan.  Every lane rolls the Gear fingerprint
-//               over its own 4 KiB run (64-byte warm-up: the masked bits only
+//   k_scan2     the byte scan.  Every lane rolls the Gear fingerprint
+//               over its own run (512 B - 8 KiB, sized so the launch fills
+//               every CU; 64-byte warm-up: the masked bits only
 //               depend on the last W <= 64 bytes), tests MaskS at every
 //               position and appends the rare hits to a candidate index of
 //               64-KiB blocks (u16 offsets).
@@ -17,9 +18,10 @@
 //               previous segment's exit until it meets a speculative chain.
 //   k_emit      one workgroup per buffer: selects the junction walks that lie
 //               on the chain from offset 0, prefix-sums and writes the
-//               (offset, length) cut list.
-//   k_fallback  sequential single-wave walker; runs only when k_emit flags a
-//               buffer it could not resolve (pathological data) or in debug.
+//               (offset, length) cut list; flags a buffer whose chains
+//               never merged (pathological data).
+//   k_seq       sequential single-wave walk for flagged buffers (and every
+//               buffer in the cross-check debug mode); exits at once otherwise.
 //
 // next(p) is wave-cooperative and decides exactly what the reference decides:
 // the truncated window [p+Min, p+Min+W-1) (fingerprint reset at p+Min) by a
@@ -369,7 +371,7 @@ struct WalkCtx {
 // First position in [lo, hi) whose fingerprint (reset to 0 before fz) hits the
 // mask, by a raw scan: lane j rolls its own 256-byte slice of a 16-KiB block
 // after a 64-byte warm-up.  Positions are buffer-relative.
-__device__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
+__device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
                                   uint32_t mlo, uint32_t mhi)
 {
     const uint64_t H = C.ub + hi, FZ = C.ub + fz;
@@ -409,17 +411,14 @@ __device__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, ui
 
 // Truncated window: positions fz + j, j < W - 1, fingerprint started at 0 at
 // fz.  fp_j = sum_{k<=j} G[b_k] << (j-k): a weighted inclusive scan over lanes.
+// `byte` is data[fz + lane], preloaded by the caller (valid lanes only).
 __device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64_t fz,
-                                    uint64_t norm_end, uint64_t lim)
+                                    uint64_t norm_end, uint64_t lim, uint32_t byte)
 {
     const uint32_t j = C.lane;
     const uint64_t pos = fz + j;
     const bool valid = (j + 1 < P.win) && pos < lim;
-    uint64_t v = 0;
-    if (valid) {
-        const uint32_t byte = reinterpret_cast<const uint8_t *>(C.ub)[pos];
-        v = lds_gear(C.tab, (byte << 8) | C.laneoff);
-    }
+    uint64_t v = valid ? lds_gear(C.tab, (byte << 8) | C.laneoff) : 0ull;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint64_t t = __shfl_up(v, d);
@@ -431,9 +430,19 @@ __device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64
     return m ? fz + uint64_t(__ffsll((unsigned long long)m) - 1) : kNoHit;
 }
 
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = __shfl_xor(v, d);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
 // First full-window MaskS candidate in [a, b), from the index.  Index blocks
 // that overflowed (dense data) are rescanned raw.
-__device__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+__device__ __noinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                     uint64_t fz)
 {
     const uint64_t blk0 = a >> kIdxShift, blk1 = (b - 1) >> kIdxShift;
@@ -470,6 +479,9 @@ __device__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64
 // The reference's (*Chunker).Next + (*FastCDC).Algorithm for the chunk that
 // starts at p: returns the next chunk start, len at the end of a final
 // stream, or kUndet when the bytes present do not decide the cut.
+// Common case in ONE global round trip: every lane issues, together, its
+// truncated-window byte, the candidate count of one index block and two
+// entries of the first two blocks.
 __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
 {
     const uint64_t E = C.len, r = E - p;
@@ -494,14 +506,51 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
     }
     const uint64_t fz = p + P.min_size;
     const uint64_t norm_end = p + norm;
-    uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim);
-    if (h != kNoHit) return h + P.cut_adj;
     const uint64_t full0 = fz + (P.win - 1);
     const uint64_t s_end = min(norm_end, lim);
-    if (full0 < s_end) {
-        h = index_first_hit(C, P, full0, s_end, fz);
-        if (h != kNoHit) return h + P.cut_adj;
+    const bool has_s = full0 < s_end;
+    const uint32_t j = C.lane;
+    // ---- fused loads
+    const uint64_t tpos = fz + j;
+    const bool tvalid = (j + 1 < P.win) && tpos < lim;
+    const uint64_t blk0 = full0 >> kIdxShift;
+    const uint64_t blk1 = has_s ? (s_end - 1) >> kIdxShift : 0;
+    const bool bin = has_s && blk0 + j <= blk1;
+    const uint64_t eblk = blk0 + (j >> 4);
+    const bool ein = has_s && j < 32 && eblk <= blk1;
+    uint32_t byte = 0, cnt = 0, epair = 0;
+    if (tvalid) byte = reinterpret_cast<const uint8_t *>(C.ub)[tpos];
+    if (bin) cnt = C.cnt[blk0 + j];
+    if (ein) epair = *reinterpret_cast<const uint32_t *>(C.ent + eblk * kIdxCap + 2u * (j & 15u));
+    // ---- truncated window [fz, fz + W - 1)
+    uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim, byte);
+    if (h != kNoHit) return h + P.cut_adj;
+    // ---- full-window MaskS candidates in [full0, s_end)
+    if (has_s) {
+        const uint32_t c0 = __shfl(cnt, 0), c1 = __shfl(cnt, 1);
+        const bool two = blk0 + 1 <= blk1;
+        if (c0 <= kIdxCap && (!two || c1 <= kIdxCap)) {
+            const uint32_t ce = j < 16 ? c0 : c1;
+            const uint32_t i0 = 2u * (j & 15u);
+            const uint64_t bs = eblk << kIdxShift;
+            uint64_t best = kNoHit;
+            if (ein) {
+                const uint64_t q0 = bs + (epair & 0xFFFFu), q1 = bs + (epair >> 16);
+                if (i0 < ce && q0 >= full0 && q0 < s_end) best = q0;
+                if (i0 + 1 < ce && q1 >= full0 && q1 < s_end && q1 < best) best = q1;
+            }
+            best = wave_min_u64(best);
+            if (best != kNoHit) return best + P.cut_adj;
+            if (blk0 + 2 <= blk1) {
+                h = index_first_hit(C, P, (blk0 + 2) << kIdxShift, s_end, fz);
+                if (h != kNoHit) return h + P.cut_adj;
+            }
+        } else {
+            h = index_first_hit(C, P, full0, s_end, fz);
+            if (h != kNoHit) return h + P.cut_adj;
+        }
     }
+    // ---- MaskL region [p + Normal, p + n): on-demand raw scan
     const uint64_t l_lo = max(norm_end, full0);
     if (l_lo < lim) {
         h = raw_first_hit(C, l_lo, lim, fz, P.ml_lo, P.ml_hi);
@@ -557,7 +606,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, c
         const uint64_t nx = next_node(C, P, p);
         if (C.lane == 0) nodes[c] = nx;
         ++c;
-        if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) break;
+        if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1 || B.debug == 3) break;
         p = nx;
     }
     if (C.lane == 0) W.w1_cnt[g] = c;
@@ -589,10 +638,16 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
         for (;;) {
             const uint64_t s = x / B.seg;
             const uint32_t gs = D.seg_base + uint32_t(s);
-            const uint32_t ns = W.w1_cnt[gs] - 1;  // speculative nodes below the segment exit
             const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
+            // the count and the first 64 speculative nodes in one round trip
+            const uint32_t ns = W.w1_cnt[gs] - 1;  // speculative nodes below the segment exit
+            const uint64_t v0 = C.lane < cap1 ? sn[C.lane] : kUndet;
             int k = -1;
-            for (uint32_t base = 0; base < ns && k < 0; base += 64) {
+            {
+                const uint64_t m = __ballot(C.lane < ns && v0 == x);
+                if (m) k = __ffsll((unsigned long long)m) - 1;
+            }
+            for (uint32_t base = 64; base < ns && k < 0; base += 64) {
                 const uint32_t i = base + C.lane;
                 const uint64_t m = __ballot(i < ns && sn[i] == x);
                 if (m) k = int(base) + __ffsll((unsigned long long)m) - 1;
@@ -625,6 +680,48 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
 }
 
 // ---------------------------------------------------------------------------
+// k_seq: sequential resolver, one workgroup per buffer.  The workgroup fills
+// the Gear table, then wave 0 walks next() from offset 0 and writes the cut
+// list.  It runs only for buffers k_emit flagged: pathological data whose
+// speculative chains never merge, and the debug mode that cross-checks the fast
+// path.  A separate kernel so that k_emit (1024 threads, 128 VGPRs) stays free
+// of the walker's register footprint; for unflagged buffers it exits at once.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSeqThreads = 256;
+
+__global__ __launch_bounds__(kSeqThreads) void k_seq(const Batch B, const DevParams P, const Workspace W)
+{
+    __shared__ uint64_t s_tab[256 * 32];
+    const uint32_t b = blockIdx.x;
+    if (!B.force_fallback && W.flags[b] == 0) return;
+    fill_gear_lds<kSeqThreads>(s_tab, W.gear);
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const BufDesc &D = B.b[b];
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    uint64_t p = 0, idx = 0;
+    while (p < C.len) {
+        const uint64_t nx = next_node(C, P, p);
+        if (nx == kUndet) break;
+        if (C.lane == 0 && idx < D.cap) {
+            cdc_cut cut;
+            cut.offset = p;
+            cut.length = uint32_t(nx - p);
+            cut.reserved = 0;
+            D.out[idx] = cut;
+        }
+        ++idx;
+        p = nx;
+    }
+    if (C.lane == 0) {
+        D.res->ncuts = idx <= D.cap ? idx : D.cap;
+        D.res->consumed = p;
+        D.res->status = idx <= D.cap ? CDC_OK : CDC_E_NOSPACE;
+        D.res->needed = idx;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_emit: one workgroup per buffer.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum, uint32_t &total)
@@ -649,7 +746,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum
     return off + incl - v;
 }
 
-__global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
+__global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P, const Workspace W)
 {
     __shared__ uint32_t s_nt[kNtCap];
     __shared__ uint32_t s_ntc[kNtCap];  // w2_conv of each listed junction
@@ -661,9 +758,9 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
     const BufDesc &D = B.b[b];
     const uint32_t NS = D.nseg, G0 = D.seg_base, cap1 = B.cap1, cap2 = B.cap2;
     const uint64_t len = D.len;
+    if (tid == 0) W.flags[b] = 0;
     if (NS == 0) {
         if (tid == 0) {
-            W.flags[b] = 0;
             D.res->ncuts = 0;
             D.res->consumed = 0;
             D.res->status = CDC_OK;
@@ -671,10 +768,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
         }
         return;
     }
-    if (B.force_fallback) {
-        if (tid == 0) W.flags[b] = 1;
-        return;
-    }
+    if (B.force_fallback) return;  // k_seq resolves every buffer
     const uint64_t e0 = W.w1_nodes[size_t(G0) * cap1 + W.w1_cnt[G0] - 1];
     const bool cont = NS > 1 && e0 != kUndet && e0 < len;
 
@@ -706,6 +800,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
             __syncthreads();
         }
     }
+    if (B.debug == 1) return;
     // Phase 2: follow the chain from segment 1 over the non-trivial junctions.
     if (tid == 0 && cont) {
         const uint32_t m = s_m;
@@ -736,10 +831,11 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
     }
     __syncthreads();
     if (s_fail) {
-        if (tid == 0) W.flags[b] = 1;
+        if (tid == 0) W.flags[b] = 1;  // k_seq resolves this buffer
         return;
     }
     const uint32_t niv = s_niv;
+    if (B.debug == 2) return;
 
     // Phase 3: per-piece node counts, prefix sum, write cuts.
     uint32_t carry = 0;
@@ -797,68 +893,41 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const Workspace W)
         if (cnt > 0) {
             const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
             uint64_t idx = uint64_t(carry) + pre;
-            for (uint32_t t = 0; t < cnt; ++t) {
-                const uint64_t pos = t < c2 ? list2[t] : sn[k + (t - c2)];
-                const uint64_t succ =
-                    t + 1 < cnt ? (t + 1 < c2 ? list2[t + 1] : sn[k + (t + 1 - c2)]) : end;
-                if (succ == kUndet) {
-                    D.res->consumed = pos;  // the last chunk is not decided yet
-                    break;
+            // nodes of the piece in batches of 8: all loads of a batch issue together
+            for (uint32_t t0 = 0; t0 < cnt; t0 += 8) {
+                uint64_t v[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    const uint32_t t = t0 + i;
+                    v[i] = t < cnt ? (t < c2 ? list2[t] : sn[k + (t - c2)]) : end;
                 }
-                if (idx < D.cap) {
-                    cdc_cut cut;
-                    cut.offset = pos;
-                    cut.length = uint32_t(succ - pos);
-                    cut.reserved = 0;
-                    D.out[idx] = cut;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t t = t0 + i;
+                    if (t >= cnt) break;
+                    const uint64_t pos = v[i], succ = v[i + 1];
+                    if (succ == kUndet) {
+                        D.res->consumed = pos;  // the last chunk is not decided yet
+                        break;
+                    }
+                    if (idx < D.cap) {
+                        cdc_cut cut;
+                        cut.offset = pos;
+                        cut.length = uint32_t(succ - pos);
+                        cut.reserved = 0;
+                        D.out[idx] = cut;
+                    }
+                    ++idx;
+                    if (succ >= len) D.res->consumed = len;
                 }
-                ++idx;
-                if (succ >= len) D.res->consumed = len;
             }
         }
         carry += tot;
     }
     if (tid == 0) {
-        W.flags[b] = 0;
         D.res->ncuts = carry <= D.cap ? carry : D.cap;
         D.res->status = carry <= D.cap ? CDC_OK : CDC_E_NOSPACE;
         D.res->needed = carry;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_fallback: sequential single-wave resolver (same next() as above).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_fallback(const Batch B, const DevParams P,
-                                                 const Workspace W)
-{
-    const uint32_t b = blockIdx.x;
-    if (W.flags[b] == 0) return;
-    __shared__ uint64_t s_tab[256 * 32];
-    fill_gear_lds<64>(s_tab, W.gear);
-    __syncthreads();
-    const BufDesc &D = B.b[b];
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
-    uint64_t p = 0, idx = 0;
-    while (p < C.len) {
-        const uint64_t nx = next_node(C, P, p);
-        if (nx == kUndet) break;
-        if (C.lane == 0 && idx < D.cap) {
-            cdc_cut cut;
-            cut.offset = p;
-            cut.length = uint32_t(nx - p);
-            cut.reserved = 0;
-            D.out[idx] = cut;
-        }
-        ++idx;
-        p = nx;
-    }
-    if (C.lane == 0) {
-        D.res->ncuts = idx <= D.cap ? idx : D.cap;
-        D.res->consumed = p;
-        D.res->status = idx <= D.cap ? CDC_OK : CDC_E_NOSPACE;
-        D.res->needed = idx;
-        W.flags[b] = 0;
     }
 }
 
@@ -938,7 +1007,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 // Optional live profiling: hipEvents recorded on the launch stream around the
 // scan kernel and around the whole pipeline of each launch group.
 struct ProfRec {
-    hipEvent_t e0, e1, e2;  // before k_scan, after k_scan, after k_fallback
+    hipEvent_t e0, e1, e2;  // before the scan, after the scan, after k_seq
     uint64_t scan_bytes;
 };
 static std::mutex g_prof_mu;
@@ -981,8 +1050,8 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
         hipLaunchKernelGGL(k_walk2, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
     }
-    hipLaunchKernelGGL(k_emit, dim3(B.nbufs), dim3(1024), 0, st, B, W);
-    hipLaunchKernelGGL(k_fallback, dim3(B.nbufs), dim3(64), 0, st, B, P, W);
+    hipLaunchKernelGGL(k_emit, dim3(B.nbufs), dim3(1024), 0, st, B, P, W);
+    hipLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, B, P, W);
     if (prof) {
         (void)hipEventRecord(pr.e2, st);
         std::lock_guard<std::mutex> lk(g_prof_mu);

@@ -224,12 +224,30 @@ def test_c3_low_entropy_1GiB(oracle):
 
 
 # ---------------------------------------------------------------- host paths / Go API mirror
-def test_chunk_buffers_host_path(oracle, monkeypatch):
-    """cdc_chunk: host buffers in, host lists out; includes a buffer larger
-    than the staging arena (streamed through it)."""
-    monkeypatch.setenv("CDC_HOST_ARENA_MB", "16")
+@pytest.mark.parametrize("group_mb,maxbuf_mb", [(None, None), (16, 16), (16, 64)])
+def test_chunk_buffers_host_path(oracle, monkeypatch, group_mb, maxbuf_mb):
+    """cdc_chunk: host buffers in, host lists out, through the two-slot staging
+    pipeline.  (16, 16): the 40 MiB buffer is chunked as a stream of windows;
+    (16, 64): it is a launch group of its own; several groups alternate slots."""
+    if group_mb:
+        monkeypatch.setenv("CDC_HOST_GROUP_MB", str(group_mb))
+        monkeypatch.setenv("CDC_HOST_MAXBUF_MB", str(maxbuf_mb))
     _lib.ensure_init()
     arrays = [random_bytes(s, 90 + i) for i, s in enumerate([0, 100, 65536, 70000, 5 << 20, 40 << 20, 1 << 20])]
+    gear = _placeholder()
+    res = chunkers.ChunkBuffers(arrays, _opts(DEF))
+    for i, a in enumerate(arrays):
+        assert_same(res[i], oracle.chunk(a, gear, **DEF), f"host buffer {i}")
+
+
+def test_chunk_buffers_many_groups(oracle, monkeypatch):
+    """More buffers than one launch group holds (32) and more bytes than the
+    group budget: groups alternate between the two pipeline slots."""
+    monkeypatch.setenv("CDC_HOST_GROUP_MB", "16")
+    _lib.ensure_init()
+    rng = np.random.default_rng(7)
+    sizes = [int(x) for x in rng.integers(0, 3 << 20, size=80)]
+    arrays = [random_bytes(sz, 500 + i) for i, sz in enumerate(sizes)]
     gear = _placeholder()
     res = chunkers.ChunkBuffers(arrays, _opts(DEF))
     for i, a in enumerate(arrays):
