@@ -267,7 +267,7 @@ def main():
                 sample.append(a)
                 tot += a.size
             sample_cuts = [np.asarray(c) for c in host_cuts[:len(sample)]]
-        else:
+        elif args.e2e_reps > 0 or not args.no_cpu_baseline:
             host = [t.cpu().numpy() for t in bufs[:1]]
             if args.e2e_reps > 0:
                 rate, sec, e2e_cuts = e2e_host_rate(chunkers, opts, host, args.e2e_reps)

@@ -209,11 +209,9 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
     W.w1_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w1_nodes);
     W.w1_cnt = reinterpret_cast<uint32_t *>(b + pl.off_w1_cnt);
     W.w2_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w2_nodes);
-    W.w2_cnt = reinterpret_cast<uint32_t *>(b + pl.off_w2_cnt);
-    W.w2_conv = reinterpret_cast<uint32_t *>(b + pl.off_w2_conv);
-    W.w2_idx = reinterpret_cast<uint32_t *>(b + pl.off_w2_idx);
-    W.w2_term = reinterpret_cast<uint64_t *>(b + pl.off_w2_term);
+    W.piece = reinterpret_cast<Piece *>(b + pl.off_piece);
     W.flags = reinterpret_cast<uint32_t *>(b + pl.off_flags);
+    W.w1_exit = reinterpret_cast<uint64_t *>(b + pl.off_w1_exit);
     W.gear = gear;
     return W;
 }
@@ -258,7 +256,7 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         D.task_base = tasks;
         segs += D.nseg;
         blks += uint32_t((lens[i] + kIdxBlock - 1) / kIdxBlock);
-        tasks += uint32_t((lens[i] + 64ull * pl.scan_lane - 1) / (64ull * pl.scan_lane));
+        tasks += uint32_t(align_tasks((lens[i] + 64ull * pl.scan_lane - 1) / (64ull * pl.scan_lane)));
     }
     const Workspace W = carve(ws, pl, ctx->d_gear);
     return launch_batch(B, P, W, stream);

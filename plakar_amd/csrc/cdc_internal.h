@@ -50,6 +50,19 @@ struct Batch {
     BufDesc b[kMaxBufsPerLaunch];
 };
 
+// The piece of the true chain that segment q contributes when the chain enters
+// it through its junction (q >= 1) or at offset 0 (q == 0): the c2 junction
+// nodes, then the speculative nodes of segment `conv` from index k on; cnt
+// nodes in all, and `end` is the node after the last one (the piece's exit).
+struct Piece {
+    uint32_t conv;  // local segment the junction walk merged into, or kConv*
+    uint32_t c2;    // junction-walk nodes (w2_nodes)
+    uint32_t k;     // merge index in segment conv's speculative chain
+    uint32_t cnt;   // nodes in the piece
+    uint64_t end;   // exit node (kUndet: undecided)
+    uint64_t pad;
+};
+
 // Device workspace, carved out of one caller-provided allocation.
 struct Workspace {
     uint32_t *blk_cnt;   // [total_blks] candidates seen per index block
@@ -57,11 +70,9 @@ struct Workspace {
     uint64_t *w1_nodes;  // [total_segs * cap1] speculative chain per segment
     uint32_t *w1_cnt;    // [total_segs]
     uint64_t *w2_nodes;  // [total_segs * cap2] junction walk per segment
-    uint32_t *w2_cnt;    // [total_segs]
-    uint32_t *w2_conv;   // [total_segs] local segment the junction walk merged into / kConv*
-    uint32_t *w2_idx;    // [total_segs] index of the merge node in that segment's chain
-    uint64_t *w2_term;   // [total_segs] terminal node when the junction walk ended the chain
+    Piece *piece;        // [total_segs] what segment q contributes if the true chain enters it
     uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "needs sequential fallback"
+    uint64_t *w1_exit;   // [total_segs] last node of the speculative chain (its exit)
     const uint64_t *gear;  // 256 entries, device copy
 };
 
@@ -74,11 +85,14 @@ struct Plan {
     uint32_t scan_lane;
     uint32_t cap1, cap2;
     uint32_t total_segs, total_blks, total_tasks;
-    size_t off_blk_cnt, off_blk_ent, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_w2_cnt,
-        off_w2_conv, off_w2_idx, off_w2_term, off_flags, bytes;
+    size_t off_blk_cnt, off_blk_ent, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_piece, off_flags,
+        off_w1_exit, bytes;
 };
 
 // Host-side helpers implemented in cdc_kernels.hip.
+// Scan tasks of one buffer, rounded up so that every buffer starts on a scan
+// workgroup boundary (k_scan2 zeroes the index blocks it owns).
+uint64_t align_tasks(uint64_t tasks);
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan);
 int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream);
 

@@ -27,6 +27,7 @@
 // the truncated window [p+Min, p+Min+W-1) (fingerprint reset at p+Min) by a
 // 64-lane weighted prefix scan, full-window MaskS hits from the index, and the
 // MaskL region [p+Normal, p+n) by an on-demand raw wave scan.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -236,6 +237,23 @@ __device__ __forceinline__ void fast_stage(const uint4 (&d)[4], uint64_t &fp, ui
 }
 
 // ---------------------------------------------------------------------------
+// Debug timestamps (B.debug & kDbgTs): s_memrealtime (100 MHz) at phase
+// boundaries, read back with cdc_debug_timestamps().  Off in production.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kDbgTs = 16;
+constexpr uint32_t kTsScan = 0;                       // 4 per scan workgroup (<= 4096)
+constexpr uint32_t kTsW1 = kTsScan + 4 * 4096;        // 8 per segment
+constexpr uint32_t kTsW2 = kTsW1 + 8 * kMaxSegs;      // 8 per segment
+constexpr uint32_t kTsEmit = kTsW2 + 8 * kMaxSegs;    // 16 for buffer 0
+constexpr uint32_t kTsSlots = kTsEmit + 16;
+__device__ uint64_t g_ts[kTsSlots];
+
+__device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
+{
+    if ((B.debug & kDbgTs) && slot < kTsSlots) g_ts[slot] = v == ~0ull ? __builtin_amdgcn_s_memrealtime() : v;
+}
+
+// ---------------------------------------------------------------------------
 // k_scan2: the same scan with coalesced LDS-DMA staging.  Each wave owns 64
 // lane segments; per 64-byte stage it issues 4 global_load_lds_dwordx4
 // (1 KiB each, every 64-B half line read whole by 4 adjacent lanes) into a
@@ -275,8 +293,30 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
                                                         const Workspace W)
 {
     __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kS2NBuf * kS2StageBytes];
+    // Zero this workgroup's candidate-index counts.  Every buffer's tasks start
+    // on a workgroup boundary and a workgroup covers 512 * scan_lane bytes (a
+    // multiple of the 64-KiB index block), so no other workgroup touches these
+    // blocks: the barrier below orders the zeroing before every append, and no
+    // separate memset launch is needed.
+    {
+        const uint32_t tw = blockIdx.x * kS2Waves + (threadIdx.x >> 6);
+        if (tw < B.total_tasks) {
+            uint32_t bw = 0;
+            while (bw + 1 < B.nbufs && tw >= B.b[bw + 1].task_base) ++bw;
+            const BufDesc &Dw = B.b[bw];
+            const uint64_t lo = uint64_t(tw - Dw.task_base) * 64u * B.scan_lane;
+            if (lo < Dw.len) {
+                const uint64_t hi = min(lo + 64ull * B.scan_lane, Dw.len);
+                uint32_t *cz = W.blk_cnt + Dw.blk_base;
+                for (uint64_t k = (lo >> kIdxShift) + (threadIdx.x & 63u); k < ((hi + kIdxBlock - 1) >> kIdxShift); k += 64)
+                    cz[k] = 0;
+            }
+        }
+    }
+    if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear);
     __syncthreads();
+    if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
     const char *tab = s_lds;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -292,6 +332,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
     const uint64_t a0 = ub & ~15ull;                  // 16-aligned base
     const uint64_t lo_ok = a0, hi_ok = (ub + D.len + 15) & ~15ull;  // safe (16-B blocks of the buffer)
     const uint64_t seg0 = uint64_t(task - D.task_base) * 64u;       // first lane segment of the task
+    if (seg0 * B.scan_lane >= D.len) return;                        // alignment padding task
     // this lane's tested range
     const uint64_t s = (seg0 + lane) * sl;
     const bool active = s < D.len;
@@ -352,6 +393,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
             }
         }
     }
+    if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
 
 // ---------------------------------------------------------------------------
@@ -588,9 +630,12 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, c
                                                                const Workspace W)
 {
     __shared__ uint64_t s_tab[256 * 32];
+    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
+    const bool l0 = (threadIdx.x & 63u) == 0;
+    if (l0) dbg_ts(B, kTsW1 + 8 * g);
     fill_gear_lds<kWalkWavesPerWG * 64>(s_tab, W.gear);
     __syncthreads();
-    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
+    if (l0) dbg_ts(B, kTsW1 + 8 * g + 1);
     if (g >= B.total_segs) return;
     const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
@@ -602,14 +647,33 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, c
     uint32_t c = 0;
     if (C.lane == 0) nodes[c] = p;
     ++c;
+    uint64_t nx;
     for (;;) {
-        const uint64_t nx = next_node(C, P, p);
-        if (C.lane == 0) nodes[c] = nx;
+        nx = next_node(C, P, p);
+        if (C.lane == 0) {
+            nodes[c] = nx;
+            if (c == 1) dbg_ts(B, kTsW1 + 8 * g + 2);
+        }
         ++c;
-        if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1 || B.debug == 3) break;
+        if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) break;
         p = nx;
     }
-    if (C.lane == 0) W.w1_cnt[g] = c;
+    if (C.lane == 0) {
+        W.w1_cnt[g] = c;
+        W.w1_exit[g] = nx;
+        if (q == 0) {  // the true chain starts here: the whole speculative chain is its piece
+            Piece pc;
+            pc.conv = 0;
+            pc.c2 = 0;
+            pc.k = 0;
+            pc.cnt = c - 1;
+            pc.end = nx;
+            pc.pad = 0;
+            W.piece[g] = pc;
+        }
+        dbg_ts(B, kTsW1 + 8 * g + 3);
+        dbg_ts(B, kTsW1 + 8 * g + 4, c);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -620,18 +684,22 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
                                                                const Workspace W)
 {
     __shared__ uint64_t s_tab[256 * 32];
+    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
+    const bool l0 = (threadIdx.x & 63u) == 0;
+    if (l0) dbg_ts(B, kTsW2 + 8 * g);
     fill_gear_lds<kWalkWavesPerWG * 64>(s_tab, W.gear);
     __syncthreads();
-    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
+    if (l0) dbg_ts(B, kTsW2 + 8 * g + 1);
     if (g >= B.total_segs) return;
     const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
     if (g == D.seg_base) return;  // segment 0 of a buffer has no junction
     const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
     const uint32_t cap1 = B.cap1;
-    const uint64_t e = W.w1_nodes[size_t(g - 1) * cap1 + W.w1_cnt[g - 1] - 1];
-    uint32_t conv = kConvNone, idx = 0, c2 = 0;
-    uint64_t term = e;
+    const uint64_t e = W.w1_exit[g - 1];
+    if (l0) dbg_ts(B, kTsW2 + 8 * g + 2, e);
+    uint32_t conv = kConvNone, idx = 0, c2 = 0, mcnt = 0;
+    uint64_t term = e, mend = 0;
     uint64_t *out = W.w2_nodes + size_t(g) * B.cap2;
     if (e != kUndet && e < C.len) {
         uint64_t x = e;
@@ -641,6 +709,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
             const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
             // the count and the first 64 speculative nodes in one round trip
             const uint32_t ns = W.w1_cnt[gs] - 1;  // speculative nodes below the segment exit
+            const uint64_t gx = W.w1_exit[gs];
             const uint64_t v0 = C.lane < cap1 ? sn[C.lane] : kUndet;
             int k = -1;
             {
@@ -655,6 +724,8 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
             if (k >= 0) {
                 conv = uint32_t(s);
                 idx = uint32_t(k);
+                mcnt = ns - uint32_t(k);
+                mend = gx;
                 break;
             }
             if (c2 >= B.cap2) {
@@ -672,10 +743,24 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
         }
     }
     if (C.lane == 0) {
-        W.w2_conv[g] = conv;
-        W.w2_idx[g] = idx;
-        W.w2_cnt[g] = c2;
-        W.w2_term[g] = term;
+        Piece pc;
+        pc.conv = conv;
+        pc.c2 = c2;
+        pc.k = idx;
+        pc.pad = 0;
+        if (conv < kConvOvf) {  // merged: junction nodes, then the speculative chain from k
+            pc.cnt = c2 + mcnt;
+            pc.end = mend;
+        } else if (conv == kConvTerm) {  // the chain ended inside the junction walk
+            pc.cnt = c2;
+            pc.end = term;
+        } else {  // kConvNone: the chain ended before this segment; kConvOvf: fallback
+            pc.cnt = 0;
+            pc.end = term;
+        }
+        W.piece[g] = pc;
+        dbg_ts(B, kTsW2 + 8 * g + 3);
+        dbg_ts(B, kTsW2 + 8 * g + 4, c2);
     }
 }
 
@@ -755,6 +840,8 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
     __shared__ uint32_t s_m, s_niv, s_fail;
 
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const bool tsb = tid == 0 && b == 0;
+    if (tsb) dbg_ts(B, kTsEmit);
     const BufDesc &D = B.b[b];
     const uint32_t NS = D.nseg, G0 = D.seg_base, cap1 = B.cap1, cap2 = B.cap2;
     const uint64_t len = D.len;
@@ -769,7 +856,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
         return;
     }
     if (B.force_fallback) return;  // k_seq resolves every buffer
-    const uint64_t e0 = W.w1_nodes[size_t(G0) * cap1 + W.w1_cnt[G0] - 1];
+    const uint64_t e0 = W.w1_exit[G0];
     const bool cont = NS > 1 && e0 != kUndet && e0 < len;
 
     // Phase 1: compact the junctions that do not simply hand over to the next segment.
@@ -785,7 +872,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
             bool nt = false;
             uint32_t c = 0;
             if (q < NS) {
-                c = W.w2_conv[G0 + q];
+                c = W.piece[G0 + q].conv;
                 nt = c >= kConvOvf || c != q;  // jump = c + 1 differs from q + 1
             }
             uint32_t tot;
@@ -800,7 +887,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
             __syncthreads();
         }
     }
-    if (B.debug == 1) return;
+    if (tsb) dbg_ts(B, kTsEmit + 1);
     // Phase 2: follow the chain from segment 1 over the non-trivial junctions.
     if (tid == 0 && cont) {
         const uint32_t m = s_m;
@@ -835,8 +922,12 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
         return;
     }
     const uint32_t niv = s_niv;
-    if (B.debug == 2) return;
 
+    if (tsb) {
+        dbg_ts(B, kTsEmit + 2);
+        dbg_ts(B, kTsEmit + 8, s_m);
+        dbg_ts(B, kTsEmit + 9, niv);
+    }
     // Phase 3: per-piece node counts, prefix sum, write cuts.
     uint32_t carry = 0;
     for (uint32_t base = 0; base < NS; base += blockDim.x) {
@@ -860,36 +951,17 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
                 valid = !(f >= 0 && q < s_ive[f]);
             }
         }
-        uint32_t c2 = 0, cnt = 0, k = 0, gs = 0;
-        uint64_t end = 0;
-        const uint64_t *list2 = nullptr;
-        if (valid) {
-            if (q == 0) {
-                cnt = W.w1_cnt[G0] - 1;
-                gs = G0;
-                k = 0;
-                end = e0;
-            } else {
-                const uint32_t c = W.w2_conv[G0 + q];
-                c2 = W.w2_cnt[G0 + q];
-                list2 = W.w2_nodes + size_t(G0 + q) * cap2;
-                if (c < kConvOvf) {
-                    gs = G0 + c;
-                    k = W.w2_idx[G0 + q];
-                    const uint32_t n1 = W.w1_cnt[gs];
-                    cnt = c2 + (n1 - 1 - k);
-                    end = W.w1_nodes[size_t(gs) * cap1 + n1 - 1];
-                } else if (c == kConvTerm) {
-                    cnt = c2;
-                    end = W.w2_term[G0 + q];
-                } else {
-                    cnt = 0;  // chain ended before this segment
-                }
-            }
-        }
+        Piece pc{};
+        if (valid) pc = W.piece[G0 + q];
+        const uint32_t c2 = pc.c2, cnt = pc.cnt, k = pc.k;
+        const uint32_t gs = G0 + (pc.conv < kConvOvf ? pc.conv : 0u);
+        const uint64_t end = pc.end;
+        const uint64_t *list2 = W.w2_nodes + size_t(G0 + q) * cap2;
         const uint32_t emit = cnt - ((cnt > 0 && end == kUndet) ? 1u : 0u);
         uint32_t tot;
+        if (tsb && base == 0) dbg_ts(B, kTsEmit + 3);
         const uint32_t pre = block_excl_scan(emit, s_wsum, tot);
+        if (tsb && base == 0) dbg_ts(B, kTsEmit + 4);
         if (cnt > 0) {
             const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
             uint64_t idx = uint64_t(carry) + pre;
@@ -924,6 +996,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
         }
         carry += tot;
     }
+    if (tsb) dbg_ts(B, kTsEmit + 5);
     if (tid == 0) {
         D.res->ncuts = carry <= D.cap ? carry : D.cap;
         D.res->status = carry <= D.cap ? CDC_OK : CDC_E_NOSPACE;
@@ -935,6 +1008,8 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
 // Host side: planning and launching.
 // ---------------------------------------------------------------------------
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint64_t align_tasks(uint64_t t) { return (t + kS2Waves - 1) / kS2Waves * kS2Waves; }
 
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 {
@@ -978,7 +1053,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     for (int i = 0; i < nbufs; ++i) {
         segs += (lens[i] + seg - 1) / seg;
         blks += (lens[i] + kIdxBlock - 1) / kIdxBlock;
-        tasks += (lens[i] + task_bytes - 1) / task_bytes;
+        tasks += align_tasks((lens[i] + task_bytes - 1) / task_bytes);
     }
     if (segs >= 0xFFFF0000ull || blks >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
     plan->total_segs = uint32_t(segs);
@@ -995,11 +1070,9 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_w1_nodes = take(segs * plan->cap1 * 8);
     plan->off_w1_cnt = take(segs * 4);
     plan->off_w2_nodes = take(segs * plan->cap2 * 8);
-    plan->off_w2_cnt = take(segs * 4);
-    plan->off_w2_conv = take(segs * 4);
-    plan->off_w2_idx = take(segs * 4);
-    plan->off_w2_term = take(segs * 8);
+    plan->off_piece = take(segs * sizeof(Piece));
     plan->off_flags = take(kMaxBufsPerLaunch * 4);
+    plan->off_w1_exit = take(segs * 8);
     plan->bytes = off;
     return CDC_OK;
 }
@@ -1037,23 +1110,30 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     for (uint32_t i = 0; i < B.nbufs; ++i) bytes += B.b[i].len;
     ProfRec pr;
     const bool prof = prof_begin(pr, bytes);
-    if (B.total_blks > 0 &&
-        hipMemsetAsync(W.blk_cnt, 0, size_t(B.total_blks) * 4, st) != hipSuccess)
-        return CDC_E_DEVICE;
-    if (prof) (void)hipEventRecord(pr.e0, st);
-    if (B.total_tasks > 0)
-        hipLaunchKernelGGL(k_scan2, dim3((B.total_tasks + kS2Waves - 1) / kS2Waves),
-                           dim3(kS2Waves * 64), 0, st, B, P, W);
-    if (prof) (void)hipEventRecord(pr.e1, st);
+    // With profiling on, the events ride on the kernels' own dispatch packets
+    // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
+    const dim3 sgrid((B.total_tasks + kS2Waves - 1) / kS2Waves), sblock(kS2Waves * 64);
+    if (B.total_tasks == 0) {  // every buffer is empty
+        if (prof) {
+            (void)hipEventRecord(pr.e0, st);
+            (void)hipEventRecord(pr.e1, st);
+        }
+    } else if (prof) {
+        hipExtLaunchKernelGGL(k_scan2, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
+    } else {
+        hipLaunchKernelGGL(k_scan2, sgrid, sblock, 0, st, B, P, W);
+    }
     if (B.total_segs > 0 && !B.force_fallback) {
         const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
         hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
         hipLaunchKernelGGL(k_walk2, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
     }
     hipLaunchKernelGGL(k_emit, dim3(B.nbufs), dim3(1024), 0, st, B, P, W);
-    hipLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, B, P, W);
+    if (prof)
+        hipExtLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, nullptr, pr.e2, 0, B, P, W);
+    else
+        hipLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, B, P, W);
     if (prof) {
-        (void)hipEventRecord(pr.e2, st);
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof_live.push_back(pr);
     }
@@ -1061,6 +1141,12 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
 }
 
 }  // namespace cdc
+
+extern "C" int cdc_debug_timestamps(uint64_t *out, uint64_t n)
+{
+    if (!out || n > cdc::kTsSlots) return CDC_E_INVALID;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(cdc::g_ts), n * 8) == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+}
 
 extern "C" int cdc_profile_enable(int on)
 {
