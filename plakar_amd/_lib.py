@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libplakar_cdc.so")
+# PLAKAR_CDC_LIB selects an alternative build of the same library (kernel
+# variants for A/B measurements, tools/variants.sh); default: the in-tree build.
+LIB_PATH = os.environ.get("PLAKAR_CDC_LIB") or os.path.join(_HERE, "_lib", "libplakar_cdc.so")
 
 CDC_OK = 0
 CDC_EOF = 1

@@ -396,6 +396,94 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
     if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
 
+// DPP helpers (in-row lane shifts, no LDS round trip; ds_bpermute-based
+// shuffles cost ~100+ cycles each on the walk's critical path).
+constexpr int kDppRowShr = 0x110;  // row_shr:n = 0x110 + n
+
+template <int N>
+__device__ __forceinline__ uint64_t dpp_shr64_zero(uint64_t v)  // lanes (j & 15) < N read 0
+{
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, uint32_t(v), kDppRowShr + N, 0xF, 0xF, true);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, uint32_t(v >> 32), kDppRowShr + N, 0xF, 0xF, true);
+    return (uint64_t(hi) << 32) | lo;
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t dpp_shr32_keep(uint32_t v)  // lanes without a source keep v
+{
+    return __builtin_amdgcn_update_dpp(v, v, kDppRowShr + N, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l)
+{
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(uint32_t(v), l));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(uint32_t(v >> 32), l));
+    return (uint64_t(hi) << 32) | lo;
+}
+
+// Wave-wide minimum of a u32, uniform result: in-row DPP min, then the 4 row minima.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x)
+{
+    x = min(x, dpp_shr32_keep<1>(x));
+    x = min(x, dpp_shr32_keep<2>(x));
+    x = min(x, dpp_shr32_keep<4>(x));
+    x = min(x, dpp_shr32_keep<8>(x));
+    // readlane returns int: compare as unsigned (0xFFFFFFFF is the "none" sentinel)
+    const uint32_t r0 = uint32_t(__builtin_amdgcn_readlane(x, 15));
+    const uint32_t r1 = uint32_t(__builtin_amdgcn_readlane(x, 31));
+    const uint32_t r2 = uint32_t(__builtin_amdgcn_readlane(x, 47));
+    const uint32_t r3 = uint32_t(__builtin_amdgcn_readlane(x, 63));
+    return min(min(r0, r1), min(r2, r3));
+}
+
+// Self-test of the wave primitives (one wave): out[0] = lanes whose DPP
+// weighted prefix differs from the serial sum, out[1] = 1 if the DPP wave
+// minimum differs from the serial minimum; out[2..5] = diagnostics.
+__global__ __launch_bounds__(64) void k_selftest_wave(const uint64_t *in, uint32_t *out)
+{
+    __shared__ uint64_t s_in[64];
+    __shared__ uint64_t s_v[64];
+    const uint32_t j = threadIdx.x;
+    uint64_t g = in[j];
+    s_in[j] = g;
+    uint64_t v = g;
+    v += dpp_shr64_zero<1>(v) << 1;
+    v += dpp_shr64_zero<2>(v) << 2;
+    v += dpp_shr64_zero<4>(v) << 4;
+    v += dpp_shr64_zero<8>(v) << 8;
+    s_v[j] = v;  // in-row result
+    {
+        const uint64_t f15 = readlane64(v, 15);
+        const uint64_t f31 = readlane64(v, 31) + (f15 << 16);
+        const uint64_t f47 = readlane64(v, 47) + (f31 << 16);
+        const uint32_t row = j >> 4;
+        const uint64_t carry = row == 0 ? 0ull : row == 1 ? f15 : row == 2 ? f31 : f47;
+        v += carry << ((j & 15u) + 1u);
+    }
+    __syncthreads();
+    uint64_t ref = 0;
+    for (uint32_t k = 0; k <= j; ++k) ref = (ref << 1) + s_in[k];
+    uint64_t rowref = 0;
+    for (uint32_t k = j & ~15u; k <= j; ++k) rowref = (rowref << 1) + s_in[k];
+    const uint32_t bad = ref != v ? 1u : 0u;
+    const uint32_t badrow = rowref != s_v[j] ? 1u : 0u;
+    // values with the top bit set (the "none" sentinel included) must compare unsigned
+    auto xv = [&](uint32_t k) { return k >= 40 ? 0xFFFFFFFFu : (uint32_t(s_in[k] >> 32) | 0x80000000u); };
+    const uint32_t m = wave_min_u32(xv(j));
+    uint32_t mref = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < 64; ++k) mref = min(mref, xv(k));
+    const uint32_t mnone = wave_min_u32(j == 63 ? 0x7FFFFFFFu : 0xFFFFFFFFu);
+    const uint64_t bb = __ballot(bad), br = __ballot(badrow);
+    if (j == 0) {
+        out[0] = uint32_t(__popcll(bb));
+        out[1] = (m != mref ? 1u : 0u) | (mnone != 0x7FFFFFFFu ? 2u : 0u);
+        out[2] = uint32_t(__popcll(br));
+        out[3] = uint32_t(br);
+        out[4] = m;
+        out[5] = mref;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Wave-cooperative next(p).
 // ---------------------------------------------------------------------------
@@ -445,14 +533,15 @@ __device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, ui
             }
         }
         const uint64_t m = __ballot(hit != kNoHit);
-        if (m) return __shfl(hit, __ffsll((unsigned long long)m) - 1) - C.ub;
+        if (m) return readlane64(hit, __ffsll((unsigned long long)m) - 1) - C.ub;
         x = bend;
     }
     return kNoHit;
 }
 
 // Truncated window: positions fz + j, j < W - 1, fingerprint started at 0 at
-// fz.  fp_j = sum_{k<=j} G[b_k] << (j-k): a weighted inclusive scan over lanes.
+// fz.  fp_j = sum_{k<=j} G[b_k] << (j-k): a weighted inclusive scan over lanes,
+// in-row by DPP (shifts 1, 2, 4, 8), then the carried prefixes of rows 0-2.
 // `byte` is data[fz + lane], preloaded by the caller (valid lanes only).
 __device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64_t fz,
                                     uint64_t norm_end, uint64_t lim, uint32_t byte)
@@ -461,25 +550,22 @@ __device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64
     const uint64_t pos = fz + j;
     const bool valid = (j + 1 < P.win) && pos < lim;
     uint64_t v = valid ? lds_gear(C.tab, (byte << 8) | C.laneoff) : 0ull;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = __shfl_up(v, d);
-        if (j >= uint32_t(d)) v += t << d;
+    v += dpp_shr64_zero<1>(v) << 1;
+    v += dpp_shr64_zero<2>(v) << 2;
+    v += dpp_shr64_zero<4>(v) << 4;
+    v += dpp_shr64_zero<8>(v) << 8;
+    {
+        const uint64_t f15 = readlane64(v, 15);
+        const uint64_t f31 = readlane64(v, 31) + (f15 << 16);
+        const uint64_t f47 = readlane64(v, 47) + (f31 << 16);
+        const uint32_t row = j >> 4;
+        const uint64_t carry = row == 0 ? 0ull : row == 1 ? f15 : row == 2 ? f31 : f47;
+        v += carry << ((j & 15u) + 1u);
     }
     const bool small = pos < norm_end;
     const uint32_t mlo = small ? P.ms_lo : P.ml_lo, mhi = small ? P.ms_hi : P.ml_hi;
     const uint64_t m = __ballot(valid && key_of(v, mlo, mhi) == 0);
     return m ? fz + uint64_t(__ffsll((unsigned long long)m) - 1) : kNoHit;
-}
-
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t o = __shfl_xor(v, d);
-        v = o < v ? o : v;
-    }
-    return v;
 }
 
 // First full-window MaskS candidate in [a, b), from the index.  Index blocks
@@ -507,7 +593,7 @@ __device__ __noinline__ uint64_t index_first_hit(const WalkCtx &C, const DevPara
         while (found | dn) {
             const int lf = found ? __ffsll((unsigned long long)found) - 1 : 64;
             const int ld = dn ? __ffsll((unsigned long long)dn) - 1 : 64;
-            if (lf < ld) return __shfl(best, lf);
+            if (lf < ld) return readlane64(best, lf);
             const uint64_t db = base + uint64_t(ld);
             const uint64_t lo = max(a, db << kIdxShift), hi = min(b, (db + 1) << kIdxShift);
             const uint64_t h = raw_first_hit(C, lo, hi, fz, P.ms_lo, P.ms_hi);
@@ -569,7 +655,8 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
     if (h != kNoHit) return h + P.cut_adj;
     // ---- full-window MaskS candidates in [full0, s_end)
     if (has_s) {
-        const uint32_t c0 = __shfl(cnt, 0), c1 = __shfl(cnt, 1);
+        const uint32_t c0 = uint32_t(__builtin_amdgcn_readlane(cnt, 0));
+        const uint32_t c1 = uint32_t(__builtin_amdgcn_readlane(cnt, 1));
         const bool two = blk0 + 1 <= blk1;
         if (c0 <= kIdxCap && (!two || c1 <= kIdxCap)) {
             const uint32_t ce = j < 16 ? c0 : c1;
@@ -581,8 +668,9 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
                 if (i0 < ce && q0 >= full0 && q0 < s_end) best = q0;
                 if (i0 + 1 < ce && q1 >= full0 && q1 < s_end && q1 < best) best = q1;
             }
-            best = wave_min_u64(best);
-            if (best != kNoHit) return best + P.cut_adj;
+            // offsets from full0 fit in 32 bits (< MaxSize <= 1 GiB)
+            const uint32_t rel = wave_min_u32(best == kNoHit ? 0xFFFFFFFFu : uint32_t(best - full0));
+            if (rel != 0xFFFFFFFFu) return full0 + rel + P.cut_adj;
             if (blk0 + 2 <= blk1) {
                 h = index_first_hit(C, P, (blk0 + 2) << kIdxShift, s_end, fz);
                 if (h != kNoHit) return h + P.cut_adj;
@@ -831,23 +919,40 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum
     return off + incl - v;
 }
 
-__global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P, const Workspace W)
+constexpr uint32_t kEmitThreads = 1024;
+constexpr uint32_t kEmitSlice = 64;     // segments written per emit workgroup
+constexpr uint32_t kEmitMaxWG = 64;     // emit workgroups per buffer
+
+__host__ __device__ inline uint32_t emit_wgs(uint32_t nseg)
+{
+    const uint32_t e = (nseg + kEmitSlice - 1) / kEmitSlice;
+    return e < 1 ? 1 : (e > kEmitMaxWG ? kEmitMaxWG : e);
+}
+
+// grid (kEmitMaxWG-capped workgroups per buffer, nbufs).  Every workgroup of a
+// buffer computes the same selection and prefix offsets (cheap, L2-resident
+// piece records); each then writes the cuts of its own slice of segments,
+// one wave per segment with lane i writing cut i (coalesced).
+__global__ __launch_bounds__(kEmitThreads) void k_emit(const Batch B, const DevParams P, const Workspace W)
 {
     __shared__ uint32_t s_nt[kNtCap];
-    __shared__ uint32_t s_ntc[kNtCap];  // w2_conv of each listed junction
+    __shared__ uint32_t s_ntc[kNtCap];  // merge segment of each listed junction
     __shared__ uint32_t s_ivs[kNtCap], s_ive[kNtCap];
+    __shared__ uint32_t s_off[kEmitSlice * 16];  // output index of the slice's segments (~0: invalid)
     __shared__ uint32_t s_wsum[16];
     __shared__ uint32_t s_m, s_niv, s_fail;
 
-    const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const bool tsb = tid == 0 && b == 0;
-    if (tsb) dbg_ts(B, kTsEmit);
+    const uint32_t b = blockIdx.y, tid = threadIdx.x;
     const BufDesc &D = B.b[b];
     const uint32_t NS = D.nseg, G0 = D.seg_base, cap1 = B.cap1, cap2 = B.cap2;
+    const uint32_t nwg = emit_wgs(NS), wg = blockIdx.x;
+    if (wg >= nwg) return;
+    const bool lead = wg == 0 && tid == 0;
+    if (lead && b == 0) dbg_ts(B, kTsEmit);
     const uint64_t len = D.len;
-    if (tid == 0) W.flags[b] = 0;
+    if (lead) W.flags[b] = 0;
     if (NS == 0) {
-        if (tid == 0) {
+        if (lead) {
             D.res->ncuts = 0;
             D.res->consumed = 0;
             D.res->status = CDC_OK;
@@ -858,6 +963,9 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
     if (B.force_fallback) return;  // k_seq resolves every buffer
     const uint64_t e0 = W.w1_exit[G0];
     const bool cont = NS > 1 && e0 != kUndet && e0 < len;
+    // this workgroup's slice of segments
+    const uint32_t per = (NS + nwg - 1) / nwg;
+    const uint32_t qa = wg * per, qb = min(NS, qa + per);
 
     // Phase 1: compact the junctions that do not simply hand over to the next segment.
     if (tid == 0) {
@@ -887,7 +995,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
             __syncthreads();
         }
     }
-    if (tsb) dbg_ts(B, kTsEmit + 1);
+    if (lead && b == 0) dbg_ts(B, kTsEmit + 1);
     // Phase 2: follow the chain from segment 1 over the non-trivial junctions.
     if (tid == 0 && cont) {
         const uint32_t m = s_m;
@@ -918,17 +1026,17 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
     }
     __syncthreads();
     if (s_fail) {
-        if (tid == 0) W.flags[b] = 1;  // k_seq resolves this buffer
+        if (lead) W.flags[b] = 1;  // k_seq resolves this buffer
         return;
     }
     const uint32_t niv = s_niv;
-
-    if (tsb) {
+    if (lead && b == 0) {
         dbg_ts(B, kTsEmit + 2);
         dbg_ts(B, kTsEmit + 8, s_m);
         dbg_ts(B, kTsEmit + 9, niv);
     }
-    // Phase 3: per-piece node counts, prefix sum, write cuts.
+
+    // Phase 3: emitted cuts per valid segment, prefix sum; keep the offsets of this slice.
     uint32_t carry = 0;
     for (uint32_t base = 0; base < NS; base += blockDim.x) {
         const uint32_t q = base + tid;
@@ -937,8 +1045,7 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
             if (q == 0) {
                 valid = true;
             } else if (cont) {
-                // binary search: last interval with start <= q
-                int lo = 0, hi = int(niv) - 1, f = -1;
+                int lo = 0, hi = int(niv) - 1, f = -1;  // last interval with start <= q
                 while (lo <= hi) {
                     const int mid = (lo + hi) >> 1;
                     if (s_ivs[mid] <= q) {
@@ -951,56 +1058,55 @@ __global__ __launch_bounds__(1024) void k_emit(const Batch B, const DevParams P,
                 valid = !(f >= 0 && q < s_ive[f]);
             }
         }
-        Piece pc{};
-        if (valid) pc = W.piece[G0 + q];
-        const uint32_t c2 = pc.c2, cnt = pc.cnt, k = pc.k;
-        const uint32_t gs = G0 + (pc.conv < kConvOvf ? pc.conv : 0u);
-        const uint64_t end = pc.end;
-        const uint64_t *list2 = W.w2_nodes + size_t(G0 + q) * cap2;
-        const uint32_t emit = cnt - ((cnt > 0 && end == kUndet) ? 1u : 0u);
+        uint32_t emit = 0;
+        if (valid) {
+            const Piece pc = W.piece[G0 + q];
+            emit = pc.cnt - ((pc.cnt > 0 && pc.end == kUndet) ? 1u : 0u);
+        }
         uint32_t tot;
-        if (tsb && base == 0) dbg_ts(B, kTsEmit + 3);
         const uint32_t pre = block_excl_scan(emit, s_wsum, tot);
-        if (tsb && base == 0) dbg_ts(B, kTsEmit + 4);
-        if (cnt > 0) {
-            const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
-            uint64_t idx = uint64_t(carry) + pre;
-            // nodes of the piece in batches of 8: all loads of a batch issue together
-            for (uint32_t t0 = 0; t0 < cnt; t0 += 8) {
-                uint64_t v[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) {
-                    const uint32_t t = t0 + i;
-                    v[i] = t < cnt ? (t < c2 ? list2[t] : sn[k + (t - c2)]) : end;
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint32_t t = t0 + i;
-                    if (t >= cnt) break;
-                    const uint64_t pos = v[i], succ = v[i + 1];
-                    if (succ == kUndet) {
-                        D.res->consumed = pos;  // the last chunk is not decided yet
-                        break;
-                    }
+        if (q >= qa && q < qb) s_off[q - qa] = valid ? carry + pre : 0xFFFFFFFFu;
+        carry += tot;
+    }
+    if (lead && b == 0) dbg_ts(B, kTsEmit + 3);
+    __syncthreads();
+
+    // Phase 4: write the slice, one wave per segment, lane i -> cut i of the piece.
+    const uint32_t lane = tid & 63u, wave = tid >> 6, nwave = blockDim.x >> 6;
+    for (uint32_t q = qa + wave; q < qb; q += nwave) {
+        const uint32_t off = s_off[q - qa];
+        if (off == 0xFFFFFFFFu) continue;
+        const Piece pc = W.piece[G0 + q];
+        const uint32_t gs = G0 + (pc.conv < kConvOvf ? pc.conv : 0u);
+        const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
+        const uint64_t *list2 = W.w2_nodes + size_t(G0 + q) * cap2;
+        for (uint32_t t0 = 0; t0 < pc.cnt; t0 += 63) {
+            const uint32_t t = t0 + lane;  // lanes 0..62 own nodes, lane 63 only feeds the successor
+            uint64_t v = pc.end;
+            if (t < pc.cnt) v = t < pc.c2 ? list2[t] : sn[pc.k + (t - pc.c2)];
+            const uint64_t succ = __shfl_down(v, 1);
+            if (lane < 63 && t < pc.cnt) {
+                const uint64_t idx = uint64_t(off) + t;
+                if (succ == kUndet) {
+                    D.res->consumed = v;  // the last chunk is not decided yet
+                } else {
                     if (idx < D.cap) {
                         cdc_cut cut;
-                        cut.offset = pos;
-                        cut.length = uint32_t(succ - pos);
+                        cut.offset = v;
+                        cut.length = uint32_t(succ - v);
                         cut.reserved = 0;
                         D.out[idx] = cut;
                     }
-                    ++idx;
                     if (succ >= len) D.res->consumed = len;
                 }
             }
         }
-        carry += tot;
     }
-    if (tsb) dbg_ts(B, kTsEmit + 5);
-    if (tid == 0) {
+    if (lead) {
         D.res->ncuts = carry <= D.cap ? carry : D.cap;
         D.res->status = carry <= D.cap ? CDC_OK : CDC_E_NOSPACE;
         D.res->needed = carry;
+        if (b == 0) dbg_ts(B, kTsEmit + 5);
     }
 }
 
@@ -1128,7 +1234,9 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
         hipLaunchKernelGGL(k_walk2, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
     }
-    hipLaunchKernelGGL(k_emit, dim3(B.nbufs), dim3(1024), 0, st, B, P, W);
+    uint32_t maxseg = 0;
+    for (uint32_t i = 0; i < B.nbufs; ++i) maxseg = B.b[i].nseg > maxseg ? B.b[i].nseg : maxseg;
+    hipLaunchKernelGGL(k_emit, dim3(emit_wgs(maxseg), B.nbufs), dim3(kEmitThreads), 0, st, B, P, W);
     if (prof)
         hipExtLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, nullptr, pr.e2, 0, B, P, W);
     else
@@ -1141,6 +1249,30 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
 }
 
 }  // namespace cdc
+
+extern "C" int cdc_selftest_wave(uint32_t *result6)
+{
+    if (!result6) return CDC_E_INVALID;
+    uint64_t h_in[64];
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto &v : h_in) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        v = x;
+    }
+    uint64_t *d_in = nullptr;
+    uint32_t *d_out = nullptr;
+    if (hipMalloc(&d_in, sizeof(h_in)) != hipSuccess) return CDC_E_DEVICE;
+    if (hipMalloc(&d_out, 6 * 4) != hipSuccess) return CDC_E_DEVICE;
+    int st = CDC_OK;
+    if (hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice) != hipSuccess) st = CDC_E_DEVICE;
+    if (st == CDC_OK) {
+        hipLaunchKernelGGL(cdc::k_selftest_wave, dim3(1), dim3(64), 0, nullptr, d_in, d_out);
+        if (hipMemcpy(result6, d_out, 6 * 4, hipMemcpyDeviceToHost) != hipSuccess) st = CDC_E_DEVICE;
+    }
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return st;
+}
 
 extern "C" int cdc_debug_timestamps(uint64_t *out, uint64_t n)
 {

@@ -309,3 +309,13 @@ def test_c4_mixed_corpus_host_path(oracle):
     gear = _placeholder()
     for i, f in enumerate(big):
         assert_same(res[i], oracle.chunk(f, gear, **DEF), f"file {i} ({f.size} B)")
+
+
+def test_wave_primitives_selftest():
+    """DPP weighted prefix scan and wave minimum used by next() vs serial sums."""
+    import ctypes
+    L = _lib.lib()
+    L.cdc_selftest_wave.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+    out = (ctypes.c_uint32 * 6)()
+    assert L.cdc_selftest_wave(out) == 0
+    assert list(out)[:3] == [0, 0, 0], list(out)

@@ -61,6 +61,10 @@ def main():
     print(f"scan WGs {len(scan)}: start {pct(us(scan[:, 0]))}")
     print(f"  fill done {pct(us(scan[:, 1]))}")
     print(f"  wave0 end {pct(us(scan[:, 2]))}")
+    idx = np.nonzero(ts[K_SCAN:K_W1].reshape(-1, 4)[:, 0] > 0)[0]
+    for x in range(8):  # blockIdx % 8 ~ XCD
+        sel = (idx % 8) == x
+        print(f"    blk%8={x}: end {pct(us(scan[sel, 2]), (0, 50, 100))}")
     nseg = int(np.count_nonzero(ts[K_W1:K_W2].reshape(-1, 8)[:, 3]))
     w1 = ts[K_W1:K_W2].reshape(-1, 8)[:nseg]
     w2 = ts[K_W2:K_EMIT].reshape(-1, 8)[:nseg]
