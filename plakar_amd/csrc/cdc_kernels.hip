@@ -185,6 +185,32 @@ __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
+#ifndef CDC_KEY_BITOP3
+#define CDC_KEY_BITOP3 1
+#endif
+// The MaskS test in the hot loop.  With the mask halves held in VGPRs the low
+// half is one VOP2 v_and_b32 (~2.3 issue cycles at 2 waves/SIMD, vs ~3.6 with
+// an SGPR operand) and the merge one v_bitop3_b32 (a & b) | c (~3.2, vs ~3.75
+// for v_and_or_b32); tools/ubench2.hip has the measurements.
+__device__ __forceinline__ uint32_t key_hot(uint64_t fp, uint32_t vmlo, uint32_t vmhi)
+{
+#if CDC_KEY_BITOP3
+    const uint32_t t = uint32_t(fp) & vmlo;
+    return __builtin_amdgcn_bitop3_b32(uint32_t(fp >> 32), vmhi, t, 0xEA);  // (hi & mhi) | t
+#else
+    return key_of(fp, vmlo, vmhi);
+#endif
+}
+
+// Copy a uniform value into a VGPR the compiler cannot fold back into an SGPR
+// operand.
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t x)
+{
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+
 __device__ __forceinline__ uint32_t roll16g(const uint64_t (&g)[16], uint64_t &fp, uint32_t mlo,
                                             uint32_t mhi)
 {
@@ -192,9 +218,9 @@ __device__ __forceinline__ uint32_t roll16g(const uint64_t (&g)[16], uint64_t &f
 #pragma unroll
     for (int k = 0; k < 16; k += 2) {
         fp = (fp << 1) + g[k];
-        const uint32_t k0 = key_of(fp, mlo, mhi);
+        const uint32_t k0 = key_hot(fp, mlo, mhi);
         fp = (fp << 1) + g[k + 1];
-        acc = umin3(acc, k0, key_of(fp, mlo, mhi));
+        acc = umin3(acc, k0, key_hot(fp, mlo, mhi));
     }
     return acc;
 }
@@ -209,12 +235,83 @@ __device__ __forceinline__ void record16g(const uint64_t (&g)[16], uint64_t f, u
     }
 }
 
+#ifndef CDC_QUARTERS
+#define CDC_QUARTERS 1
+#endif
+// Fold 4 bytes (quarter q of a 16-byte group) into fp and the running min of keys.
+template <int Q>
+__device__ __forceinline__ void roll4g(const uint64_t (&g)[16], uint64_t &fp, uint32_t &acc,
+                                       uint32_t mlo, uint32_t mhi)
+{
+#pragma unroll
+    for (int k = 4 * Q; k < 4 * Q + 4; k += 2) {
+        fp = (fp << 1) + g[k];
+        const uint32_t k0 = key_hot(fp, mlo, mhi);
+        fp = (fp << 1) + g[k + 1];
+        acc = umin3(acc, k0, key_hot(fp, mlo, mhi));
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ void gather4(uint64_t (&g)[16], const uint4 &d, const char *tab, uint32_t laneoff)
+{
+#pragma unroll
+    for (int k = 4 * Q; k < 4 * Q + 4; ++k) g[k] = lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+}
+
+// Roll group `cur` while gathering the next group into `nxt`, a quarter at a
+// time: the lgkmcnt counter saturates at 15, so with a whole group of 16
+// gathers issued ahead the first wait would also retire freshly issued ones.
+// Interleaved by quarters every forced completion is an old gather.
+__device__ __forceinline__ uint32_t roll_gather(const uint64_t (&cur)[16], uint64_t &fp, uint64_t (&nxt)[16],
+                                                const uint4 *dn, const char *tab, uint32_t laneoff,
+                                                uint32_t mlo, uint32_t mhi)
+{
+    uint32_t acc = 0xFFFFFFFFu;
+    if (dn) gather4<0>(nxt, *dn, tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    roll4g<0>(cur, fp, acc, mlo, mhi);
+    __builtin_amdgcn_sched_barrier(0);
+    if (dn) gather4<1>(nxt, *dn, tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    roll4g<1>(cur, fp, acc, mlo, mhi);
+    __builtin_amdgcn_sched_barrier(0);
+    if (dn) gather4<2>(nxt, *dn, tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    roll4g<2>(cur, fp, acc, mlo, mhi);
+    __builtin_amdgcn_sched_barrier(0);
+    if (dn) gather4<3>(nxt, *dn, tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    roll4g<3>(cur, fp, acc, mlo, mhi);
+    __builtin_amdgcn_sched_barrier(0);
+    return acc;
+}
+
 // One interior 64-byte stage (4 groups, all positions tested), gathers one group ahead.
 __device__ __forceinline__ void fast_stage(const uint4 (&d)[4], uint64_t &fp, uint64_t pos0,
                                            const char *tab, uint32_t laneoff, uint32_t mlo,
                                            uint32_t mhi, uint32_t *cnt, uint16_t *ent)
 {
     uint64_t ga[16], gb[16];
+#if CDC_QUARTERS
+    gather16(ga, d[0], tab, laneoff);
+    __builtin_amdgcn_sched_barrier(0);
+    uint64_t f0 = fp;
+    if (roll_gather(ga, fp, gb, &d[1], tab, laneoff, mlo, mhi) == 0) [[unlikely]]
+        record16g(ga, f0, pos0, mlo, mhi, cnt, ent);
+    __builtin_amdgcn_sched_barrier(0);
+    f0 = fp;
+    if (roll_gather(gb, fp, ga, &d[2], tab, laneoff, mlo, mhi) == 0) [[unlikely]]
+        record16g(gb, f0, pos0 + 16, mlo, mhi, cnt, ent);
+    __builtin_amdgcn_sched_barrier(0);
+    f0 = fp;
+    if (roll_gather(ga, fp, gb, &d[3], tab, laneoff, mlo, mhi) == 0) [[unlikely]]
+        record16g(ga, f0, pos0 + 32, mlo, mhi, cnt, ent);
+    __builtin_amdgcn_sched_barrier(0);
+    f0 = fp;
+    if (roll_gather(gb, fp, ga, nullptr, tab, laneoff, mlo, mhi) == 0) [[unlikely]]
+        record16g(gb, f0, pos0 + 48, mlo, mhi, cnt, ent);
+#else
     gather16(ga, d[0], tab, laneoff);
     __builtin_amdgcn_sched_barrier(0);
     gather16(gb, d[1], tab, laneoff);
@@ -234,6 +331,30 @@ __device__ __forceinline__ void fast_stage(const uint4 (&d)[4], uint64_t &fp, ui
     __builtin_amdgcn_sched_barrier(0);
     f0 = fp;
     if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 48, mlo, mhi, cnt, ent);
+#endif
+}
+
+// One interior stage of G 16-byte groups (all positions tested), gathers one group ahead.
+template <int G>
+__device__ __forceinline__ void fast_stage_g(const uint4 (&d)[G], uint64_t &fp, uint64_t pos0,
+                                             const char *tab, uint32_t laneoff, uint32_t mlo,
+                                             uint32_t mhi, uint32_t *cnt, uint16_t *ent)
+{
+    if constexpr (G == 4) {
+        fast_stage(d, fp, pos0, tab, laneoff, mlo, mhi, cnt, ent);
+    } else {
+        static_assert(G == 2, "groups per stage");
+        uint64_t ga[16], gb[16];
+        gather16(ga, d[0], tab, laneoff);
+        __builtin_amdgcn_sched_barrier(0);
+        gather16(gb, d[1], tab, laneoff);
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t f0 = fp;
+        if (roll16g(ga, fp, mlo, mhi) == 0) [[unlikely]] record16g(ga, f0, pos0, mlo, mhi, cnt, ent);
+        __builtin_amdgcn_sched_barrier(0);
+        f0 = fp;
+        if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 16, mlo, mhi, cnt, ent);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -261,11 +382,31 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 // ds_read_b128 through an XOR swizzle (piece k of segment s at slot
 // k ^ ((s >> 2) & 3)) that makes the reads bank-conflict-free.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kS2Waves = 8;
-constexpr uint32_t kS2Stage = 64;                     // bytes per lane per stage
-constexpr uint32_t kS2NBuf = 3;                       // ring depth (2 stages in flight)
+#ifndef CDC_SCAN_WAVES
+#define CDC_SCAN_WAVES 12
+#endif
+#ifndef CDC_SCAN_NBUF
+#define CDC_SCAN_NBUF 2
+#endif
+constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;  // waves per scan workgroup (one workgroup per CU)
+#ifndef CDC_SCAN_STAGE
+#define CDC_SCAN_STAGE 64
+#endif
+constexpr uint32_t kS2Stage = CDC_SCAN_STAGE;         // bytes per lane per stage (32 or 64)
+constexpr uint32_t kS2L = kS2Stage / 16;              // 16-B chunks per lane per stage = DMA pieces per stage
+static_assert(kS2Stage == 32 || kS2Stage == 64, "stage size");
+constexpr uint32_t kS2NBuf = CDC_SCAN_NBUF;           // ring depth (kS2NBuf - 1 stages in flight)
 constexpr uint32_t kS2StageBytes = 64u * kS2Stage;    // per wave per stage
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
+static_assert(kS2NBuf >= 2 && kS2NBuf <= 3, "ring depth");
+static_assert(kGearLdsBytes + kS2Waves * kS2NBuf * kS2StageBytes <= 160u * 1024u, "LDS budget");
+// Scan lane lengths are multiples of kLaneQuant, so that one workgroup covers
+// whole 64-KiB index blocks (k_scan2 zeroes the blocks it owns).
+constexpr uint32_t lane_quant(uint32_t q)
+{
+    return (kS2Waves * 64u * q) % 65536u == 0 ? q : lane_quant(2 * q);
+}
+constexpr uint32_t kLaneQuant = lane_quant(128);
 
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
 {
@@ -284,9 +425,19 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
 {
+    static_assert(N == 0 || N == 2 || N == 4 || N == 8, "vmcnt");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// XOR swizzle of a lane's 16-B chunks inside its stage slot that makes the
+// consumer's ds_read_b128 bank-conflict-free for the gfx950 lane groups (the
+// DMA writes lane-linear, so the producer applies it to the source address).
+__device__ __forceinline__ uint32_t stage_swz(uint64_t q)
+{
+    return kS2L == 4 ? uint32_t((q >> 2) & 3u) : uint32_t((q >> 3) & 1u);
 }
 
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const DevParams P,
@@ -338,23 +489,26 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
     const bool active = s < D.len;
     const uint64_t e = active ? min(s + sl, D.len) : s;
     const uint64_t as = ub + s, ae = ub + e;
-    // stage t of segment q covers [S(q) + 64 t, +64), S(q) = align16(ub + q*sl) - 64
-    const uint32_t T = uint32_t((sl + 64u + (ub & 15u) + 63u) / 64u);
-    // the 4 segments whose pieces this lane loads: q_j = seg0 + 16 j + lane / 4
-    uint64_t src[4];
+    // stage t of segment q covers [S(q) + kS2Stage t, +kS2Stage), S(q) = align16(ub + q*sl) - 64
+    const uint32_t T = uint32_t((sl + 64u + (ub & 15u) + kS2Stage - 1u) / kS2Stage);
+    // the kS2L segments whose chunks this lane loads: q_j = seg0 + (64 / kS2L) j + lane / kS2L
+    uint64_t src[kS2L];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint64_t q = seg0 + 16u * j + (lane >> 2);
-        const uint32_t k = (lane & 3u) ^ uint32_t((q >> 2) & 3u);
+    for (uint32_t j = 0; j < kS2L; ++j) {
+        const uint64_t q = seg0 + (64u / kS2L) * j + lane / kS2L;
+        const uint32_t k = (lane % kS2L) ^ stage_swz(q - seg0);
         src[j] = ((ub + q * sl) & ~15ull) - 64u + 16u * k;
     }
     const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes +
                           wave * kS2NBuf * kS2StageBytes;
     auto issue = [&](uint32_t t) {
+#if CDC_DIAG_NO_DMA
+        if (t >= kS2NBuf) return;  // diagnostic: compute over the first ring fill again and again
+#endif
         const uint32_t dst = ring + (t % kS2NBuf) * kS2StageBytes;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint64_t g = src[j] + 64ull * t;
+        for (uint32_t j = 0; j < kS2L; ++j) {
+            uint64_t g = src[j] + uint64_t(kS2Stage) * t;
             if (g < lo_ok || g >= hi_ok) g = lo_ok;   // warm-up before byte 0 / past the end: ignored bytes
             glds16(reinterpret_cast<const void *>(g), dst + 1024u * j);
         }
@@ -362,33 +516,43 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
     uint32_t *cnt = W.blk_cnt + D.blk_base;
     uint16_t *ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
     const uint32_t mlo = P.ms_lo, mhi = P.ms_hi;
+#if CDC_KEY_BITOP3
+    const uint32_t vmlo = to_vgpr(mlo), vmhi = to_vgpr(mhi);
+#else
+    const uint32_t vmlo = mlo, vmhi = mhi;
+#endif
     const uint64_t S = ((ub + s) & ~15ull) - 64u;
-    const uint32_t swz = (lane >> 2) & 3u;
+    const uint32_t swz = stage_swz(lane);
 
+    constexpr uint32_t kAhead = kS2NBuf - 1;  // stages in flight
     uint64_t fp = 0;
-    issue(0);
-    if (T > 1) issue(1);
+    for (uint32_t t = 0; t < kAhead && t < T; ++t) issue(t);
     for (uint32_t t = 0; t < T; ++t) {
-        if (t + 2 < T) {
+        if (t + kAhead < T) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot being refilled are done
-            issue(t + 2);
-            wait_vmcnt<8>();
-        } else if (t + 1 < T) {
-            wait_vmcnt<4>();
+            issue(t + kAhead);
+            wait_vmcnt<kS2L * kAhead>();
+        } else if (kAhead == 2 && t + 1 < T) {
+            wait_vmcnt<kS2L>();
         } else {
             wait_vmcnt<0>();
         }
         if (active) {
-            const char *buf = s_lds + kGearLdsBytes + (wave * kS2NBuf + t % kS2NBuf) * kS2StageBytes + lane * 64u;
-            uint4 d[4];
+            const char *buf = s_lds + kGearLdsBytes + (wave * kS2NBuf + t % kS2NBuf) * kS2StageBytes + lane * kS2Stage;
+            uint4 d[kS2L];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
-            const uint64_t st0 = S + 64ull * t;
-            if (st0 >= as && st0 + 64 <= ae) {
-                fast_stage(d, fp, st0 - ub, tab, laneoff, mlo, mhi, cnt, ent);
+            for (uint32_t g = 0; g < kS2L; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+            const uint64_t st0 = S + uint64_t(kS2Stage) * t;
+#if CDC_DIAG_NO_COMPUTE
+            fp += d[0].x ^ d[kS2L - 1].w;
+            if (fp == 0x123456789ull) index_append(cnt, ent, 0);
+            continue;
+#endif
+            if (st0 >= as && st0 + kS2Stage <= ae) {
+                fast_stage_g<kS2L>(d, fp, st0 - ub, tab, laneoff, vmlo, vmhi, cnt, ent);
             } else {
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
+                for (uint32_t g = 0; g < kS2L; ++g)
                     scan_group(d[g], fp, st0 + 16u * g, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
             }
         }
@@ -473,7 +637,9 @@ __global__ __launch_bounds__(64) void k_selftest_wave(const uint64_t *in, uint32
     uint32_t mref = 0xFFFFFFFFu;
     for (uint32_t k = 0; k < 64; ++k) mref = min(mref, xv(k));
     const uint32_t mnone = wave_min_u32(j == 63 ? 0x7FFFFFFFu : 0xFFFFFFFFu);
-    const uint64_t bb = __ballot(bad), br = __ballot(badrow);
+    const uint32_t ba = uint32_t(g), bbv = uint32_t(g >> 32), bc = uint32_t(g >> 16);
+    const uint32_t b3bad = __builtin_amdgcn_bitop3_b32(ba, bbv, bc, 0xEA) != ((ba & bbv) | bc) ? 1u : 0u;
+    const uint64_t bb = __ballot(bad | (b3bad << 1)), br = __ballot(badrow);
     if (j == 0) {
         out[0] = uint32_t(__popcll(bb));
         out[1] = (m != mref ? 1u : 0u) | (mnone != 0x7FFFFFFFu ? 2u : 0u);
@@ -1121,7 +1287,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 {
     uint64_t maxlen = 0;
     for (int i = 0; i < nbufs; ++i) maxlen = lens[i] > maxlen ? lens[i] : maxlen;
-    uint64_t mult = 8;
+    uint64_t mult = 16;
     if (const char *env = getenv("CDC_SEG_MULT")) {
         const long v = atol(env);
         if (v >= 2 && v <= 1024) mult = uint64_t(v);
@@ -1143,13 +1309,13 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
         return uint64_t(n);
     }();
     uint64_t want = (total + cus * kS2Waves * 64 - 1) / (cus * kS2Waves * 64);
-    want = (want + 127) & ~127ull;
-    if (want < 512) want = 512;
-    if (want > kScanLaneBytes) want = kScanLaneBytes;
+    want = (want + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
+    if (want < 512) want = (512 + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
+    if (want > kScanLaneBytes) want = kScanLaneBytes / kLaneQuant * kLaneQuant;
     uint32_t lane = uint32_t(want);
     if (const char *env = getenv("CDC_SCAN_LANE_BYTES")) {
         const long v = atol(env);
-        if (v >= 256 && v <= (1 << 20) && v % 128 == 0) lane = uint32_t(v);
+        if (v >= 256 && v <= (1 << 20) && v % kLaneQuant == 0) lane = uint32_t(v);
     }
     plan->scan_lane = lane;
     const uint64_t task_bytes = 64ull * lane;
