@@ -112,6 +112,10 @@ DevParams make_params(const cdc_opts *o)
     P.cut_adj = g.cut_adj;
     const uint64_t m = g.mask_s | g.mask_l;
     P.win = 64u - uint32_t(__builtin_clzll(m));
+    P.fs_sh = uint32_t(__builtin_clzll(g.mask_s));  // 63 - highest MaskS bit
+    const uint64_t ms = g.mask_s << P.fs_sh;
+    P.fs_lo = uint32_t(ms);
+    P.fs_hi = uint32_t(ms >> 32);
     return P;
 }
 

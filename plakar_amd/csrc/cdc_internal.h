@@ -24,6 +24,9 @@ struct DevParams {
     uint32_t ms_lo, ms_hi, ml_lo, ml_hi;  // MaskS / MaskL split in 32-bit halves
     uint32_t cut_adj;                     // 0: cut at i, 1: cut at i + 1
     uint32_t win;                         // W = highest mask bit + 1 (window length)
+    // The scan's shifted frame: fp' = fp << fs_sh (fs_sh = 63 - highest MaskS
+    // bit) and MaskS << fs_sh split in 32-bit halves (k_scan).
+    uint32_t fs_sh, fs_lo, fs_hi;
 };
 
 struct BufDesc {
@@ -91,7 +94,7 @@ struct Plan {
 
 // Host-side helpers implemented in cdc_kernels.hip.
 // Scan tasks of one buffer, rounded up so that every buffer starts on a scan
-// workgroup boundary (k_scan2 zeroes the index blocks it owns).
+// workgroup boundary (k_scan zeroes the index blocks it owns).
 uint64_t align_tasks(uint64_t tasks);
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan);
 int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream);

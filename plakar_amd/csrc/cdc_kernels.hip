@@ -49,20 +49,25 @@ static constexpr uint32_t kNtCap = 4096;        // emit: non-trivial junctions p
 // Byte address of entry b for this lane = (b << 8) | ((lane & 31) << 3),
 // built from the packed data word by one v_perm_b32.
 // ---------------------------------------------------------------------------
-// NT threads fill the 32-copy table: thread t owns copy (t & 31) of entries
-// (t >> 5) + k * NT/32; all its global loads are issued before any store.
+// NT threads fill the 32-copy table (entry e, copy c at index 32 e + c),
+// optionally in the scan's shifted frame.  Any NT: 8192 slots are strided over
+// the block (the global loads of the 2-KiB table hit L2 / L1).
 template <int NT>
-__device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gear)
+__device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gear, uint32_t sh = 0)
 {
-    static_assert(NT % 32 == 0 && NT >= 64, "block size");
-    constexpr int kPer = 256 * 32 / NT;
-    constexpr int kStep = NT / 32;
-    const uint32_t c = threadIdx.x & 31u, e0 = threadIdx.x >> 5;
+    static_assert(NT % 64 == 0, "block size");
+    constexpr int kPer = (256 * 32 + NT - 1) / NT;
     uint64_t v[kPer];
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) v[i] = gear[e0 + i * kStep];
+    for (int i = 0; i < kPer; ++i) {
+        const uint32_t x = threadIdx.x + uint32_t(i) * NT;
+        v[i] = x < 8192u ? gear[x >> 5] : 0;
+    }
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) tab[(e0 + i * kStep) * 32 + c] = v[i];
+    for (int i = 0; i < kPer; ++i) {
+        const uint32_t x = threadIdx.x + uint32_t(i) * NT;
+        if (x < 8192u) tab[x] = v[i] << sh;
+    }
 }
 
 __device__ __forceinline__ uint64_t lds_gear(const char *tab, uint32_t addr)
@@ -375,12 +380,35 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 }
 
 // ---------------------------------------------------------------------------
-// k_scan2: the same scan with coalesced LDS-DMA staging.  Each wave owns 64
-// lane segments; per 64-byte stage it issues 4 global_load_lds_dwordx4
-// (1 KiB each, every 64-B half line read whole by 4 adjacent lanes) into a
-// private 3-deep LDS ring, and each lane reads its own 64 bytes back with
-// ds_read_b128 through an XOR swizzle (piece k of segment s at slot
-// k ^ ((s >> 2) & 3)) that makes the reads bank-conflict-free.
+// k_scan: the byte scan.  Each wave owns 64 lane runs of B.scan_lane bytes;
+// per stage of kStage bytes per lane it issues kL global_load_lds_dwordx4
+// (1 KiB each; every 64-B line half read whole by adjacent lanes) into a
+// private kNBuf-deep LDS ring, and each lane reads its own kStage bytes back
+// with ds_read_b128 through an XOR swizzle (piece p of lane c at slot
+// p ^ stage_swz(c)) that makes the reads bank-conflict-free.
+//
+// The fingerprint runs in a shifted frame: the LDS Gear table holds
+// G[b] << sh with sh = 63 - (highest MaskS bit), so fp' = fp << sh keeps every
+// fp bit the masks can see (bits 0..hb) and the high dword of fp' holds the
+// top 32 of them.  The hot test per byte is one v_and of that dword with the
+// shifted MaskS high half (13 of the 15 default MaskS bits): a necessary
+// condition, reduced by v_min3 to one branch per 16 bytes.  A group whose
+// filter fired (2^-13 per byte at the default masks) is re-rolled exactly
+// (all mask bits, and the lane's [s, e) bounds), so warm-up bytes, bytes past
+// the lane's run and lanes past the buffer's end need no separate code path:
+// every stage of every lane runs the same straight-line loop.
+//
+// Software pipeline, per wave: the DMA of stage t + kNBuf - 1 is issued at the
+// top of stage t into the slot stage t - 1 vacated; the next stage's data is
+// read (ds_read_b128) at the start of the current stage's last group, and the
+// next group's 16 Gear gathers are issued a quarter at a time into the
+// registers the current group's roll has just consumed.
+//
+// DMA addressing: one wave-uniform 64-bit base (SGPR pair) and one 32-bit
+// per-lane offset per piece, advanced by kStage per stage and clamped to the
+// buffer's last 16-byte block (v_add + v_min per piece), so the warm-up before
+// byte 0 and the ragged end read in-bounds bytes that the exact recheck then
+// ignores.
 // ---------------------------------------------------------------------------
 #ifndef CDC_SCAN_WAVES
 #define CDC_SCAN_WAVES 12
@@ -388,67 +416,124 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 #ifndef CDC_SCAN_NBUF
 #define CDC_SCAN_NBUF 2
 #endif
-constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;  // waves per scan workgroup (one workgroup per CU)
 #ifndef CDC_SCAN_STAGE
 #define CDC_SCAN_STAGE 64
 #endif
-constexpr uint32_t kS2Stage = CDC_SCAN_STAGE;         // bytes per lane per stage (32 or 64)
-constexpr uint32_t kS2L = kS2Stage / 16;              // 16-B chunks per lane per stage = DMA pieces per stage
-static_assert(kS2Stage == 32 || kS2Stage == 64, "stage size");
-constexpr uint32_t kS2NBuf = CDC_SCAN_NBUF;           // ring depth (kS2NBuf - 1 stages in flight)
-constexpr uint32_t kS2StageBytes = 64u * kS2Stage;    // per wave per stage
+constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
+constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
+constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane per stage = DMAs per stage
+constexpr uint32_t kGroups = kStage / 16;             // 16-byte groups per stage
+static_assert(kStage == 32 || kStage == 64, "stage size");
+constexpr uint32_t kNBuf = CDC_SCAN_NBUF;             // ring depth (kNBuf - 1 stages in flight)
+constexpr uint32_t kAhead = kNBuf - 1;
+constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
-static_assert(kS2NBuf >= 2 && kS2NBuf <= 3, "ring depth");
-static_assert(kGearLdsBytes + kS2Waves * kS2NBuf * kS2StageBytes <= 160u * 1024u, "LDS budget");
+static_assert(kNBuf >= 2 && kNBuf <= 3, "ring depth");
+static_assert(kGearLdsBytes + kS2Waves * kNBuf * kStageBytes <= 160u * 1024u, "LDS budget");
 // Scan lane lengths are multiples of kLaneQuant, so that one workgroup covers
-// whole 64-KiB index blocks (k_scan2 zeroes the blocks it owns).
+// whole 64-KiB index blocks (k_scan zeroes the blocks it owns).
 constexpr uint32_t lane_quant(uint32_t q)
 {
     return (kS2Waves * 64u * q) % 65536u == 0 ? q : lane_quant(2 * q);
 }
 constexpr uint32_t kLaneQuant = lane_quant(128);
 
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
-{
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
 {
-    static_assert(N == 0 || N == 2 || N == 4 || N == 8, "vmcnt");
+    static_assert(N >= 0 && N <= 8, "vmcnt");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else static_assert(N == 0, "vmcnt value");
 }
 
-// XOR swizzle of a lane's 16-B chunks inside its stage slot that makes the
+// XOR swizzle of a lane's 16-B pieces inside its stage slot that makes the
 // consumer's ds_read_b128 bank-conflict-free for the gfx950 lane groups (the
 // DMA writes lane-linear, so the producer applies it to the source address).
-__device__ __forceinline__ uint32_t stage_swz(uint64_t q)
+__device__ __forceinline__ uint32_t stage_swz(uint32_t c)
 {
-    return kS2L == 4 ? uint32_t((q >> 2) & 3u) : uint32_t((q >> 3) & 1u);
+    return kL == 4 ? ((c >> 2) & 3u) : ((c >> 3) & 1u);
 }
 
-__global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const DevParams P,
-                                                        const Workspace W)
+// One stage's kL LDS-DMA pieces in ONE asm statement: M0 is written and read
+// inside it (and restored), every VGPR offset is read before the statement
+// ends (trailing s_nop guards the compiler's next write of those registers).
+#ifndef CDC_DMA_NOPS
+#define CDC_DMA_NOPS 0
+#endif
+#if CDC_DMA_NOPS
+#define DMA_PAD "s_nop 7\n\ts_nop 7\n\t"
+#else
+#define DMA_PAD ""
+#endif
+__device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uint32_t (&off)[kL])
 {
-    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kS2NBuf * kS2StageBytes];
+    uint32_t keep;
+    if constexpr (kL == 4) {
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %6\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, %5\n\t" DMA_PAD
+            "s_add_u32 m0, m0, 0x400\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %2, %5\n\t" DMA_PAD
+            "s_add_u32 m0, m0, 0x400\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %3, %5\n\t" DMA_PAD
+            "s_add_u32 m0, m0, 0x400\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %4, %5\n\t" DMA_PAD
+            "s_mov_b32 m0, %0\n\t"
+            "s_nop 1"
+            : "=&s"(keep)
+            : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "s"(base), "s"(dst)
+            : "memory", "scc");
+    } else {
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %4\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, %3\n\t"
+            "s_add_u32 m0, m0, 0x400\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %2, %3\n\t"
+            "s_mov_b32 m0, %0\n\t"
+            "s_nop 1"
+            : "=&s"(keep)
+            : "v"(off[0]), "v"(off[1]), "s"(base), "s"(dst)
+            : "memory", "scc");
+    }
+}
+
+// Exact MaskS test of one 16-byte group in the shifted frame, from fp' before
+// the group; positions outside the lane's run [s, e) are ignored.  Re-gathers
+// the group's Gear values (the hot path's registers already hold the next
+// group's).  Rare: runs when the hi-dword filter fired somewhere in the wave.
+__device__ __forceinline__ void recheck_group(uint64_t f, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                           int64_t pos0, int64_t s, int64_t e, const char *tab, uint32_t laneoff,
+                                           uint32_t xlo, uint32_t xhi, uint32_t *cnt, uint16_t *ent)
+{
+    const uint32_t w[4] = {w0, w1, w2, w3};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        f = (f << 1) + lds_gear(tab, gear_addr(laneoff, w[k >> 2], k));
+        const int64_t pos = pos0 + k;
+        if (((uint32_t(f) & xlo) | (uint32_t(f >> 32) & xhi)) == 0 && pos >= s && pos < e)
+            index_append(cnt, ent, uint64_t(pos));
+    }
+}
+
+__global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
+{
+    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kNBuf * kStageBytes];
     // Zero this workgroup's candidate-index counts.  Every buffer's tasks start
-    // on a workgroup boundary and a workgroup covers 512 * scan_lane bytes (a
-    // multiple of the 64-KiB index block), so no other workgroup touches these
-    // blocks: the barrier below orders the zeroing before every append, and no
-    // separate memset launch is needed.
+    // on a workgroup boundary and a workgroup covers kS2Waves * 64 * scan_lane
+    // bytes (a multiple of the 64-KiB index block), so no other workgroup
+    // touches these blocks: the barrier below orders the zeroing before every
+    // append, and no separate memset launch is needed.
     {
         const uint32_t tw = blockIdx.x * kS2Waves + (threadIdx.x >> 6);
         if (tw < B.total_tasks) {
@@ -465,7 +550,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
         }
     }
     if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
-    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear);
+    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, P.fs_sh);
     __syncthreads();
     if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
     const char *tab = s_lds;
@@ -480,82 +565,98 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan2(const Batch B, const De
 
     const uint64_t sl = B.scan_lane;                  // multiple of 128
     const uint64_t ub = reinterpret_cast<uint64_t>(D.data);
-    const uint64_t a0 = ub & ~15ull;                  // 16-aligned base
-    const uint64_t lo_ok = a0, hi_ok = (ub + D.len + 15) & ~15ull;  // safe (16-B blocks of the buffer)
-    const uint64_t seg0 = uint64_t(task - D.task_base) * 64u;       // first lane segment of the task
-    if (seg0 * B.scan_lane >= D.len) return;                        // alignment padding task
-    // this lane's tested range
-    const uint64_t s = (seg0 + lane) * sl;
-    const bool active = s < D.len;
-    const uint64_t e = active ? min(s + sl, D.len) : s;
-    const uint64_t as = ub + s, ae = ub + e;
-    // stage t of segment q covers [S(q) + kS2Stage t, +kS2Stage), S(q) = align16(ub + q*sl) - 64
-    const uint32_t T = uint32_t((sl + 64u + (ub & 15u) + kS2Stage - 1u) / kS2Stage);
-    // the kS2L segments whose chunks this lane loads: q_j = seg0 + (64 / kS2L) j + lane / kS2L
-    uint64_t src[kS2L];
+    const uint64_t lo_ok = ub & ~15ull, hi_ok = (ub + D.len + 15) & ~15ull;  // 16-B blocks of the buffer
+    const uint64_t seg0 = uint64_t(task - D.task_base) * 64u;               // first lane run of the task
+    if (seg0 * sl >= D.len) return;                                          // alignment padding task
+    // this lane's tested range [s, e), buffer-relative
+    const int64_t s = int64_t((seg0 + lane) * sl);
+    const int64_t e = s < int64_t(D.len) ? min(s + int64_t(sl), int64_t(D.len)) : s;
+    // stage t of lane c covers [A(c) - 64 + kStage t, + kStage), A(c) = align16(ub + (seg0 + c) sl)
+    const uint32_t T = uint32_t((sl + 64u + (ub & 15u) + kStage - 1u) / kStage);
+    const uint64_t wb = ((ub + seg0 * sl) & ~15ull) - 64u;   // lane 0's first stage
+    const uint64_t base = wb > lo_ok ? wb : lo_ok;           // wave-uniform DMA base
+    const uint64_t limw = hi_ok - 16u - base;                // last in-bounds piece (lane 0 is in bounds)
+    const uint32_t lim = limw > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(limw);
+    // the kL pieces this lane loads: DMA j carries piece (lane % kL) ^ swz of run q = seg0 + (64/kL) j + lane/kL
+    uint32_t off[kL];
 #pragma unroll
-    for (uint32_t j = 0; j < kS2L; ++j) {
-        const uint64_t q = seg0 + (64u / kS2L) * j + lane / kS2L;
-        const uint32_t k = (lane % kS2L) ^ stage_swz(q - seg0);
-        src[j] = ((ub + q * sl) & ~15ull) - 64u + 16u * k;
+    for (uint32_t j = 0; j < kL; ++j) {
+        const uint64_t q = seg0 + (64u / kL) * j + lane / kL;
+        const uint32_t k = (lane % kL) ^ stage_swz(uint32_t(q - seg0));
+        off[j] = uint32_t((((ub + q * sl) & ~15ull) - 64u + 16u * k) - base);  // wraps below base: clamped
     }
-    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes +
-                          wave * kS2NBuf * kS2StageBytes;
+    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kNBuf * kStageBytes;
     auto issue = [&](uint32_t t) {
-#if CDC_DIAG_NO_DMA
-        if (t >= kS2NBuf) return;  // diagnostic: compute over the first ring fill again and again
-#endif
-        const uint32_t dst = ring + (t % kS2NBuf) * kS2StageBytes;
+        uint32_t eff[kL];
 #pragma unroll
-        for (uint32_t j = 0; j < kS2L; ++j) {
-            uint64_t g = src[j] + uint64_t(kS2Stage) * t;
-            if (g < lo_ok || g >= hi_ok) g = lo_ok;   // warm-up before byte 0 / past the end: ignored bytes
-            glds16(reinterpret_cast<const void *>(g), dst + 1024u * j);
-        }
+        for (uint32_t j = 0; j < kL; ++j) eff[j] = min(off[j] + kStage * t, lim);
+        dma_stage(base, ring + (t % kNBuf) * kStageBytes, eff);
+    };
+    auto slot_of = [&](uint32_t t) -> const char * {
+        return s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + lane * kStage;
     };
     uint32_t *cnt = W.blk_cnt + D.blk_base;
     uint16_t *ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
-    const uint32_t mlo = P.ms_lo, mhi = P.ms_hi;
-#if CDC_KEY_BITOP3
-    const uint32_t vmlo = to_vgpr(mlo), vmhi = to_vgpr(mhi);
-#else
-    const uint32_t vmlo = mlo, vmhi = mhi;
-#endif
-    const uint64_t S = ((ub + s) & ~15ull) - 64u;
+    const uint32_t vhi = to_vgpr(P.fs_hi);
+    const uint32_t xlo = P.fs_lo, xhi = P.fs_hi;
     const uint32_t swz = stage_swz(lane);
+    // buffer-relative position of this lane's first staged byte
+    const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - 64u) - int64_t(ub);
 
-    constexpr uint32_t kAhead = kS2NBuf - 1;  // stages in flight
-    uint64_t fp = 0;
     for (uint32_t t = 0; t < kAhead && t < T; ++t) issue(t);
+    wait_vmcnt<kL * (kAhead - 1)>();
+    uint4 d[kGroups];
+    {
+        const char *buf = slot_of(0);
+#pragma unroll
+        for (uint32_t g = 0; g < kGroups; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+    }
+    uint64_t gv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gv[k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
+    uint64_t fp = 0;
     for (uint32_t t = 0; t < T; ++t) {
-        if (t + kAhead < T) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot being refilled are done
-            issue(t + kAhead);
-            wait_vmcnt<kS2L * kAhead>();
-        } else if (kAhead == 2 && t + 1 < T) {
-            wait_vmcnt<kS2L>();
-        } else {
-            wait_vmcnt<0>();
-        }
-        if (active) {
-            const char *buf = s_lds + kGearLdsBytes + (wave * kS2NBuf + t % kS2NBuf) * kS2StageBytes + lane * kS2Stage;
-            uint4 d[kS2L];
+        if (t + kAhead < T) issue(t + kAhead);
+        uint4 dn[kGroups];
 #pragma unroll
-            for (uint32_t g = 0; g < kS2L; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
-            const uint64_t st0 = S + uint64_t(kS2Stage) * t;
-#if CDC_DIAG_NO_COMPUTE
-            fp += d[0].x ^ d[kS2L - 1].w;
-            if (fp == 0x123456789ull) index_append(cnt, ent, 0);
-            continue;
+        for (uint32_t gi = 0; gi < kGroups; ++gi) {
+            if (gi + 1 == kGroups) {
+                // next stage's data: landed once at most kAhead - 1 younger stages are in flight
+                if (t + kAhead < T) wait_vmcnt<kL * (kAhead - 1)>();
+                else wait_vmcnt<0>();
+#if CDC_RAW_DELAY
+                asm volatile("s_sleep 2" ::: "memory");
 #endif
-            if (st0 >= as && st0 + kS2Stage <= ae) {
-                fast_stage_g<kS2L>(d, fp, st0 - ub, tab, laneoff, vmlo, vmhi, cnt, ent);
-            } else {
+#if CDC_RAW_BARRIER
+                __builtin_amdgcn_s_barrier();
+#endif
+                const char *buf = slot_of(t + 1);
 #pragma unroll
-                for (uint32_t g = 0; g < kS2L; ++g)
-                    scan_group(d[g], fp, st0 + 16u * g, as, ae, ub, tab, laneoff, mlo, mhi, cnt, ent);
+                for (uint32_t g = 0; g < kGroups; ++g) dn[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
             }
+            const uint4 &nx = gi + 1 < kGroups ? d[gi + 1] : dn[0];
+            const uint64_t f0 = fp;
+            uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int k = 4 * q; k < 4 * q + 4; k += 2) {
+                    fp = (fp << 1) + gv[k];
+                    const uint32_t k0 = uint32_t(fp >> 32) & vhi;
+                    fp = (fp << 1) + gv[k + 1];
+                    acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 4 * q; k < 4 * q + 4; ++k) gv[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (acc == 0) [[unlikely]]
+                recheck_group(f0, d[gi].x, d[gi].y, d[gi].z, d[gi].w, rel0 + int64_t(kStage * t + 16u * gi), s, e,
+                              tab, laneoff, xlo, xhi, cnt, ent);
         }
+#pragma unroll
+        for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
     }
     if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
@@ -1391,9 +1492,9 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
             (void)hipEventRecord(pr.e1, st);
         }
     } else if (prof) {
-        hipExtLaunchKernelGGL(k_scan2, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
+        hipExtLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
     } else {
-        hipLaunchKernelGGL(k_scan2, sgrid, sblock, 0, st, B, P, W);
+        hipLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, B, P, W);
     }
     if (B.total_segs > 0 && !B.force_fallback) {
         const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
