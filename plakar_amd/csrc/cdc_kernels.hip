@@ -468,6 +468,11 @@ __device__ __forceinline__ uint32_t stage_swz(uint32_t c)
 #else
 #define DMA_PAD ""
 #endif
+#if CDC_DMA_NT
+#define DMA_AUX " nt"
+#else
+#define DMA_AUX ""
+#endif
 __device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uint32_t (&off)[kL])
 {
     uint32_t keep;
@@ -476,16 +481,16 @@ __device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uin
             "s_mov_b32 %0, m0\n\t"
             "s_mov_b32 m0, %6\n\t"
             "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, %5\n\t" DMA_PAD
+            "global_load_lds_dwordx4 %1, %5" DMA_AUX "\n\t" DMA_PAD
             "s_add_u32 m0, m0, 0x400\n\t"
             "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %2, %5\n\t" DMA_PAD
+            "global_load_lds_dwordx4 %2, %5" DMA_AUX "\n\t" DMA_PAD
             "s_add_u32 m0, m0, 0x400\n\t"
             "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %3, %5\n\t" DMA_PAD
+            "global_load_lds_dwordx4 %3, %5" DMA_AUX "\n\t" DMA_PAD
             "s_add_u32 m0, m0, 0x400\n\t"
             "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %4, %5\n\t" DMA_PAD
+            "global_load_lds_dwordx4 %4, %5" DMA_AUX "\n\t" DMA_PAD
             "s_mov_b32 m0, %0\n\t"
             "s_nop 1"
             : "=&s"(keep)
@@ -508,21 +513,54 @@ __device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uin
     }
 }
 
-// Exact MaskS test of one 16-byte group in the shifted frame, from fp' before
-// the group; positions outside the lane's run [s, e) are ignored.  Re-gathers
-// the group's Gear values (the hot path's registers already hold the next
-// group's).  Rare: runs when the hi-dword filter fired somewhere in the wave.
-__device__ __forceinline__ void recheck_group(uint64_t f, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
-                                           int64_t pos0, int64_t s, int64_t e, const char *tab, uint32_t laneoff,
-                                           uint32_t xlo, uint32_t xhi, uint32_t *cnt, uint16_t *ent)
+// Hits found by the scan are held in two per-lane registers and appended to
+// the candidate index after the lane's last stage: a returning global atomic
+// waits (vmcnt) for every older vector-memory operation, i.e. for the stages
+// in flight, so appends inside the loop would drain the DMA pipeline.  A third
+// hit in one lane run (rare on random data; every byte on degenerate data)
+// is appended at once.
+struct PendingHits {
+    uint64_t slots = 0;  // up to two u32 run-relative positions
+    uint32_t n = 0;
+};
+
+__device__ __forceinline__ void record_hit(PendingHits &ph, int32_t r, int64_t s, uint32_t *cnt, uint16_t *ent)
 {
-    const uint32_t w[4] = {w0, w1, w2, w3};
+#if CDC_DIAG_NO_APPEND
+    if (r != 0x7FFFFFF0) return;
+#endif
+    if (ph.n < 2) {
+        ph.slots |= uint64_t(uint32_t(r)) << (32 * ph.n);
+        ++ph.n;
+    } else {
+        index_append(cnt, ent, uint64_t(s + r));
+    }
+}
+
+// Exact MaskS test of one 16-byte group in the shifted frame, from fp' before
+// the group and the group's 16 Gear values; r0 is the group's first position
+// relative to the lane's run start, whose length is len (positions outside
+// [0, len) are warm-up or past the run and are ignored).  Runs when the
+// hi-dword filter fired in some lane of the wave (2^-13 per byte at the
+// default masks), exec-masked to those lanes.
+__device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16], int32_t r0, int32_t len,
+                                           uint32_t xlo, uint32_t xhi, PendingHits &ph, int64_t s, uint32_t *cnt,
+                                           uint16_t *ent)
+{
+    uint32_t key[16];
+    uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        f = (f << 1) + lds_gear(tab, gear_addr(laneoff, w[k >> 2], k));
-        const int64_t pos = pos0 + k;
-        if (((uint32_t(f) & xlo) | (uint32_t(f >> 32) & xhi)) == 0 && pos >= s && pos < e)
-            index_append(cnt, ent, uint64_t(pos));
+        f = (f << 1) + g[k];
+        key[k] = __builtin_amdgcn_bitop3_b32(uint32_t(f >> 32), xhi, uint32_t(f) & xlo, 0xEA);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) m = umin3(m, key[k], key[k + 1]);
+    if (m != 0) return;  // filter false positive (3 in 4 at the default masks)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int32_t r = r0 + k;
+        if (key[k] == 0 && r >= 0 && r < len) record_hit(ph, r, s, cnt, ent);
     }
 }
 
@@ -587,6 +625,9 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     }
     const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kNBuf * kStageBytes;
     auto issue = [&](uint32_t t) {
+#if CDC_DIAG_NO_DMA
+        if (t >= kNBuf) return;  // diagnostic: compute over the first ring fill again and again
+#endif
         uint32_t eff[kL];
 #pragma unroll
         for (uint32_t j = 0; j < kL; ++j) eff[j] = min(off[j] + kStage * t, lim);
@@ -603,61 +644,85 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     // buffer-relative position of this lane's first staged byte
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - 64u) - int64_t(ub);
 
-    for (uint32_t t = 0; t < kAhead && t < T; ++t) issue(t);
-    wait_vmcnt<kL * (kAhead - 1)>();
+    // Every stage's data is copied into registers (d / dn) before its slot is
+    // needed again, so slot t % kNBuf is refilled with stage t + kNBuf as soon
+    // as stage t's reads have retired (after group 0 of stage t): kNBuf stages
+    // in flight per wave with a kNBuf-slot ring.
+    for (uint32_t t = 0; t < kNBuf && t < T; ++t) issue(t);
+    if (T > kAhead) wait_vmcnt<kL * kAhead>();
+    else wait_vmcnt<0>();
     uint4 d[kGroups];
     {
         const char *buf = slot_of(0);
 #pragma unroll
         for (uint32_t g = 0; g < kGroups; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+        asm volatile("" ::: "memory");  // the slot reads issue before any gather (see the lgkmcnt below)
     }
-    uint64_t gv[16];
+    // gathers double-buffered by group parity: group gi rolls gv[gi & 1] while
+    // the next group's values land in gv[(gi + 1) & 1]; a recheck reads the
+    // rolled group's values from registers.
+    uint64_t gv[2][16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) gv[k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
+    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
     uint64_t fp = 0;
+    PendingHits ph;
+    const int32_t len = int32_t(e - s);
+    const int32_t rr0 = int32_t(rel0 - s);  // run-relative position of the lane's first staged byte
     for (uint32_t t = 0; t < T; ++t) {
-        if (t + kAhead < T) issue(t + kAhead);
         uint4 dn[kGroups];
 #pragma unroll
         for (uint32_t gi = 0; gi < kGroups; ++gi) {
+            if (gi == 1 && t + kNBuf < T) {
+                // >= 16 gathers were issued after stage t's slot reads: lgkmcnt(15)
+                // retires those reads, and the slot can take stage t + kNBuf.
+                asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+                issue(t + kNBuf);
+            }
             if (gi + 1 == kGroups) {
-                // next stage's data: landed once at most kAhead - 1 younger stages are in flight
-                if (t + kAhead < T) wait_vmcnt<kL * (kAhead - 1)>();
+                // next stage's data: landed once at most kNBuf - 1 younger stages are in flight
+                if (t + kNBuf < T) wait_vmcnt<kL * kAhead>();
                 else wait_vmcnt<0>();
-#if CDC_RAW_DELAY
-                asm volatile("s_sleep 2" ::: "memory");
-#endif
-#if CDC_RAW_BARRIER
-                __builtin_amdgcn_s_barrier();
-#endif
                 const char *buf = slot_of(t + 1);
 #pragma unroll
                 for (uint32_t g = 0; g < kGroups; ++g) dn[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+                asm volatile("" ::: "memory");
             }
             const uint4 &nx = gi + 1 < kGroups ? d[gi + 1] : dn[0];
+            uint64_t (&cur)[16] = gv[gi & 1];
+            uint64_t (&nxt)[16] = gv[(gi + 1) & 1];
+#if CDC_DIAG_NO_COMPUTE
+            fp += nx.x ^ d[gi].w;  // diagnostic: staging only
+            if (fp == 0x123456789ull) index_append(cnt, ent, 0);
+            continue;
+#endif
             const uint64_t f0 = fp;
             uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
 #pragma unroll
                 for (int k = 4 * q; k < 4 * q + 4; k += 2) {
-                    fp = (fp << 1) + gv[k];
+                    fp = (fp << 1) + cur[k];
                     const uint32_t k0 = uint32_t(fp >> 32) & vhi;
-                    fp = (fp << 1) + gv[k + 1];
+                    fp = (fp << 1) + cur[k + 1];
                     acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
                 }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int k = 4 * q; k < 4 * q + 4; ++k) gv[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
+                for (int k = 4 * q; k < 4 * q + 4; ++k) nxt[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
                 __builtin_amdgcn_sched_barrier(0);
             }
+#if CDC_DIAG_NO_RECHECK
+            if (acc == 0x12345) [[unlikely]]
+#else
             if (acc == 0) [[unlikely]]
-                recheck_group(f0, d[gi].x, d[gi].y, d[gi].z, d[gi].w, rel0 + int64_t(kStage * t + 16u * gi), s, e,
-                              tab, laneoff, xlo, xhi, cnt, ent);
+#endif
+                recheck_group(f0, cur, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, ph, s, cnt, ent);
         }
 #pragma unroll
         for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
     }
+    // the pending hits (up to two per lane)
+    for (uint32_t k = 0; k < ph.n; ++k) index_append(cnt, ent, uint64_t(s + int32_t(uint32_t(ph.slots >> (32 * k)))));
     if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
 
