@@ -414,7 +414,7 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 #define CDC_SCAN_WAVES 12
 #endif
 #ifndef CDC_SCAN_NBUF
-#define CDC_SCAN_NBUF 2
+#define CDC_SCAN_NBUF 1
 #endif
 #ifndef CDC_SCAN_STAGE
 #define CDC_SCAN_STAGE 64
@@ -423,12 +423,12 @@ constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgrou
 constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
 constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane per stage = DMAs per stage
 constexpr uint32_t kGroups = kStage / 16;             // 16-byte groups per stage
-static_assert(kStage == 32 || kStage == 64, "stage size");
+static_assert(kStage == 32 || kStage == 64 || kStage == 128, "stage size");
 constexpr uint32_t kNBuf = CDC_SCAN_NBUF;             // ring depth (kNBuf - 1 stages in flight)
 constexpr uint32_t kAhead = kNBuf - 1;
 constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
-static_assert(kNBuf >= 2 && kNBuf <= 3, "ring depth");
+static_assert(kNBuf >= 1 && kNBuf <= 3, "ring depth");
 static_assert(kGearLdsBytes + kS2Waves * kNBuf * kStageBytes <= 160u * 1024u, "LDS budget");
 // Scan lane lengths are multiples of kLaneQuant, so that one workgroup covers
 // whole 64-KiB index blocks (k_scan zeroes the blocks it owns).
@@ -441,8 +441,9 @@ constexpr uint32_t kLaneQuant = lane_quant(128);
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
 {
-    static_assert(N >= 0 && N <= 8, "vmcnt");
+    static_assert(N >= 0 && N <= 16, "vmcnt");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -454,7 +455,9 @@ __device__ __forceinline__ void wait_vmcnt()
 // DMA writes lane-linear, so the producer applies it to the source address).
 __device__ __forceinline__ uint32_t stage_swz(uint32_t c)
 {
-    return kL == 4 ? ((c >> 2) & 3u) : ((c >> 3) & 1u);
+    // kL pieces per lane, lane groups of ds_read_b128 (MI355X_MICROARCH.md LDS table):
+    // each group's lanes must cover distinct (bank-quad) slots.
+    return kL == 8 ? ((c >> 1) & 7u) : kL == 4 ? ((c >> 2) & 3u) : ((c >> 3) & 1u);
 }
 
 // One stage's kL LDS-DMA pieces in ONE asm statement: M0 is written and read
@@ -473,43 +476,34 @@ __device__ __forceinline__ uint32_t stage_swz(uint32_t c)
 #else
 #define DMA_AUX ""
 #endif
+#define DMA_PIECE(i) "global_load_lds_dwordx4 %" #i ", %[base]" DMA_AUX "\n\t" DMA_PAD
+#define DMA_NEXT "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
 __device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uint32_t (&off)[kL])
 {
     uint32_t keep;
-    if constexpr (kL == 4) {
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %6\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, %5" DMA_AUX "\n\t" DMA_PAD
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %2, %5" DMA_AUX "\n\t" DMA_PAD
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %3, %5" DMA_AUX "\n\t" DMA_PAD
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %4, %5" DMA_AUX "\n\t" DMA_PAD
-            "s_mov_b32 m0, %0\n\t"
-            "s_nop 1"
-            : "=&s"(keep)
-            : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "s"(base), "s"(dst)
-            : "memory", "scc");
+    if constexpr (kL == 8) {
+        asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+                     DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4) DMA_NEXT
+                     DMA_PIECE(5) DMA_NEXT DMA_PIECE(6) DMA_NEXT DMA_PIECE(7) DMA_NEXT DMA_PIECE(8)
+                     "s_mov_b32 m0, %[keep]\n\ts_nop 1"
+                     : [keep] "=&s"(keep)
+                     : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
+                       "v"(off[7]), [base] "s"(base), [dst] "s"(dst)
+                     : "memory", "scc");
+    } else if constexpr (kL == 4) {
+        asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+                     DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4)
+                     "s_mov_b32 m0, %[keep]\n\ts_nop 1"
+                     : [keep] "=&s"(keep)
+                     : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), [base] "s"(base), [dst] "s"(dst)
+                     : "memory", "scc");
     } else {
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %4\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, %3\n\t"
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %2, %3\n\t"
-            "s_mov_b32 m0, %0\n\t"
-            "s_nop 1"
-            : "=&s"(keep)
-            : "v"(off[0]), "v"(off[1]), "s"(base), "s"(dst)
-            : "memory", "scc");
+        asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+                     DMA_PIECE(1) DMA_NEXT DMA_PIECE(2)
+                     "s_mov_b32 m0, %[keep]\n\ts_nop 1"
+                     : [keep] "=&s"(keep)
+                     : "v"(off[0]), "v"(off[1]), [base] "s"(base), [dst] "s"(dst)
+                     : "memory", "scc");
     }
 }
 
