@@ -49,26 +49,42 @@ static constexpr uint32_t kNtCap = 4096;        // emit: non-trivial junctions p
 // Byte address of entry b for this lane = (b << 8) | ((lane & 31) << 3),
 // built from the packed data word by one v_perm_b32.
 // ---------------------------------------------------------------------------
-// NT threads fill the 32-copy table (entry e, copy c at index 32 e + c),
-// optionally in the scan's shifted frame.  Any NT: 8192 slots are strided over
-// the block (the global loads of the 2-KiB table hit L2 / L1).
-template <int NT>
+// NT threads fill a COPIES-copy table (entry e, copy c at index COPIES e + c),
+// optionally in the scan's shifted frame.  Any NT: the 256 * COPIES slots are
+// strided over the block (the global loads of the 2-KiB table hit L2 / L1).
+// The walkers use 8 copies (16 KiB; they are latency-bound and tolerate a few
+// bank conflicts), so a walker workgroup fits beside a scan workgroup on a CU.
+template <int NT, int COPIES = 32>
 __device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gear, uint32_t sh = 0)
 {
     static_assert(NT % 64 == 0, "block size");
-    constexpr int kPer = (256 * 32 + NT - 1) / NT;
+    constexpr uint32_t kSlots = 256u * COPIES;
+    constexpr int kPer = int((kSlots + NT - 1) / NT);
     uint64_t v[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
         const uint32_t x = threadIdx.x + uint32_t(i) * NT;
-        v[i] = x < 8192u ? gear[x >> 5] : 0;
+        v[i] = x < kSlots ? gear[x / COPIES] : 0;
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
         const uint32_t x = threadIdx.x + uint32_t(i) * NT;
-        if (x < 8192u) tab[x] = v[i] << sh;
+        if (x < kSlots) tab[x] = v[i] << sh;
     }
 }
+// Walker register cap: the scan holds 3 waves x 112 VGPRs per SIMD, so a
+// walker wave fits beside it (and one batch's resolution runs beside the next
+// batch's scan) only at <= 176 VGPRs (512 - 336).
+#ifndef CDC_WALK_WPE
+#define CDC_WALK_WPE 0
+#endif
+#if CDC_WALK_WPE
+#define CDC_WALK_ATTR __attribute__((amdgpu_waves_per_eu(CDC_WALK_WPE)))
+#else
+#define CDC_WALK_ATTR
+#endif
+constexpr uint32_t kWCopies = 8;    // walker table copies
+constexpr uint32_t kWEntShift = 6;  // log2(kWCopies * 8): bytes per walker table entry
 
 __device__ __forceinline__ uint64_t lds_gear(const char *tab, uint32_t addr)
 {
@@ -79,6 +95,12 @@ __device__ __forceinline__ uint32_t gear_addr(uint32_t laneoff, uint32_t word, i
 {
     // v_perm_b32: byte0 <- laneoff.byte0 (sel 4), byte1 <- word.byte(k), bytes 2,3 <- 0 (sel 0x0C)
     return __builtin_amdgcn_perm(laneoff, word, 0x0C0C0004u | (uint32_t(k & 3) << 8));
+}
+
+// Walker table address of byte k of word: (byte << kWEntShift) | ((lane & 7) << 3).
+__device__ __forceinline__ uint32_t wgear_addr(uint32_t wlaneoff, uint32_t word, int k)
+{
+    return (__builtin_amdgcn_ubfe(word, uint32_t(k & 3) * 8u, 8u) << kWEntShift) | wlaneoff;
 }
 
 __device__ __forceinline__ uint32_t key_of(uint64_t fp, uint32_t mlo, uint32_t mhi)
@@ -99,7 +121,7 @@ __device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, co
     uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        fp = (fp << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+        fp = (fp << 1) + lds_gear(tab, wgear_addr(laneoff, word_of(d, k >> 2), k));
         acc = min(acc, key_of(fp, mlo, mhi));
     }
     return acc;
@@ -110,7 +132,7 @@ __device__ __forceinline__ void roll16(const uint4 &d, uint64_t &fp, const char 
 {
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-        fp = (fp << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+        fp = (fp << 1) + lds_gear(tab, wgear_addr(laneoff, word_of(d, k >> 2), k));
 }
 
 // General 16-byte group at absolute address a: positions < fz have fp = 0
@@ -125,7 +147,7 @@ __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const uint64_t pos = a + k;
-        const uint64_t g = lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+        const uint64_t g = lds_gear(tab, wgear_addr(laneoff, word_of(d, k >> 2), k));
         fp = pos < fz ? 0ull : (fp << 1) + g;
         if (hit == kNoHit && pos >= ts && pos < te && pos >= fz && key_of(fp, mlo, mhi) == 0)
             hit = pos;
@@ -143,46 +165,6 @@ __device__ __forceinline__ void index_append(uint32_t *cnt, uint16_t *ent, uint6
     if (slot < kIdxCap) ent[blk * kIdxCap + slot] = uint16_t(pos & (kIdxBlock - 1));
 }
 
-__device__ __forceinline__ void scan_group(const uint4 &d, uint64_t &fp, uint64_t ga, uint64_t as,
-                                           uint64_t ae, uint64_t ub, const char *tab,
-                                           uint32_t laneoff, uint32_t mlo, uint32_t mhi,
-                                           uint32_t *cnt, uint16_t *ent)
-{
-    if (ga >= ae) return;
-    if (ga >= as && ga + 16 <= ae) {
-        const uint64_t fp0 = fp;
-        if (roll16_test(d, fp, tab, laneoff, mlo, mhi) == 0) {
-            // rare: record every hit of the group
-            uint64_t f = fp0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                f = (f << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
-                if (key_of(f, mlo, mhi) == 0) index_append(cnt, ent, ga + k - ub);
-            }
-        }
-    } else if (ga + 16 <= as) {
-        roll16(d, fp, tab, laneoff);  // warm-up
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t pos = ga + k;
-            fp = (fp << 1) + lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
-            if (pos >= as && pos < ae && key_of(fp, mlo, mhi) == 0)
-                index_append(cnt, ent, pos - ub);
-        }
-    }
-}
-
-// Software-pipelined form of the inner loop: the 16 Gear values of a group
-// are gathered (ds_read_b64) one group ahead of the multiply-free rolling
-// chain that consumes them, so LDS latency is not exposed per byte.
-__device__ __forceinline__ void gather16(uint64_t (&g)[16], const uint4 &d, const char *tab,
-                                         uint32_t laneoff)
-{
-#pragma unroll
-    for (int k = 0; k < 16; ++k) g[k] = lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
-}
-
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
 {
     uint32_t r;
@@ -190,176 +172,13 @@ __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
-#ifndef CDC_KEY_BITOP3
-#define CDC_KEY_BITOP3 1
-#endif
-// The MaskS test in the hot loop.  With the mask halves held in VGPRs the low
-// half is one VOP2 v_and_b32 (~2.3 issue cycles at 2 waves/SIMD, vs ~3.6 with
-// an SGPR operand) and the merge one v_bitop3_b32 (a & b) | c (~3.2, vs ~3.75
-// for v_and_or_b32); tools/ubench2.hip has the measurements.
-__device__ __forceinline__ uint32_t key_hot(uint64_t fp, uint32_t vmlo, uint32_t vmhi)
-{
-#if CDC_KEY_BITOP3
-    const uint32_t t = uint32_t(fp) & vmlo;
-    return __builtin_amdgcn_bitop3_b32(uint32_t(fp >> 32), vmhi, t, 0xEA);  // (hi & mhi) | t
-#else
-    return key_of(fp, vmlo, vmhi);
-#endif
-}
-
 // Copy a uniform value into a VGPR the compiler cannot fold back into an SGPR
-// operand.
+// operand (VOP2 forms with a VGPR mask issue faster than with an SGPR one).
 __device__ __forceinline__ uint32_t to_vgpr(uint32_t x)
 {
     uint32_t v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
     return v;
-}
-
-__device__ __forceinline__ uint32_t roll16g(const uint64_t (&g)[16], uint64_t &fp, uint32_t mlo,
-                                            uint32_t mhi)
-{
-    uint32_t acc = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        fp = (fp << 1) + g[k];
-        const uint32_t k0 = key_hot(fp, mlo, mhi);
-        fp = (fp << 1) + g[k + 1];
-        acc = umin3(acc, k0, key_hot(fp, mlo, mhi));
-    }
-    return acc;
-}
-
-__device__ __forceinline__ void record16g(const uint64_t (&g)[16], uint64_t f, uint64_t pos0,
-                                          uint32_t mlo, uint32_t mhi, uint32_t *cnt, uint16_t *ent)
-{
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        f = (f << 1) + g[k];
-        if (key_of(f, mlo, mhi) == 0) index_append(cnt, ent, pos0 + k);
-    }
-}
-
-#ifndef CDC_QUARTERS
-#define CDC_QUARTERS 1
-#endif
-// Fold 4 bytes (quarter q of a 16-byte group) into fp and the running min of keys.
-template <int Q>
-__device__ __forceinline__ void roll4g(const uint64_t (&g)[16], uint64_t &fp, uint32_t &acc,
-                                       uint32_t mlo, uint32_t mhi)
-{
-#pragma unroll
-    for (int k = 4 * Q; k < 4 * Q + 4; k += 2) {
-        fp = (fp << 1) + g[k];
-        const uint32_t k0 = key_hot(fp, mlo, mhi);
-        fp = (fp << 1) + g[k + 1];
-        acc = umin3(acc, k0, key_hot(fp, mlo, mhi));
-    }
-}
-
-template <int Q>
-__device__ __forceinline__ void gather4(uint64_t (&g)[16], const uint4 &d, const char *tab, uint32_t laneoff)
-{
-#pragma unroll
-    for (int k = 4 * Q; k < 4 * Q + 4; ++k) g[k] = lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
-}
-
-// Roll group `cur` while gathering the next group into `nxt`, a quarter at a
-// time: the lgkmcnt counter saturates at 15, so with a whole group of 16
-// gathers issued ahead the first wait would also retire freshly issued ones.
-// Interleaved by quarters every forced completion is an old gather.
-__device__ __forceinline__ uint32_t roll_gather(const uint64_t (&cur)[16], uint64_t &fp, uint64_t (&nxt)[16],
-                                                const uint4 *dn, const char *tab, uint32_t laneoff,
-                                                uint32_t mlo, uint32_t mhi)
-{
-    uint32_t acc = 0xFFFFFFFFu;
-    if (dn) gather4<0>(nxt, *dn, tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    roll4g<0>(cur, fp, acc, mlo, mhi);
-    __builtin_amdgcn_sched_barrier(0);
-    if (dn) gather4<1>(nxt, *dn, tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    roll4g<1>(cur, fp, acc, mlo, mhi);
-    __builtin_amdgcn_sched_barrier(0);
-    if (dn) gather4<2>(nxt, *dn, tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    roll4g<2>(cur, fp, acc, mlo, mhi);
-    __builtin_amdgcn_sched_barrier(0);
-    if (dn) gather4<3>(nxt, *dn, tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    roll4g<3>(cur, fp, acc, mlo, mhi);
-    __builtin_amdgcn_sched_barrier(0);
-    return acc;
-}
-
-// One interior 64-byte stage (4 groups, all positions tested), gathers one group ahead.
-__device__ __forceinline__ void fast_stage(const uint4 (&d)[4], uint64_t &fp, uint64_t pos0,
-                                           const char *tab, uint32_t laneoff, uint32_t mlo,
-                                           uint32_t mhi, uint32_t *cnt, uint16_t *ent)
-{
-    uint64_t ga[16], gb[16];
-#if CDC_QUARTERS
-    gather16(ga, d[0], tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    uint64_t f0 = fp;
-    if (roll_gather(ga, fp, gb, &d[1], tab, laneoff, mlo, mhi) == 0) [[unlikely]]
-        record16g(ga, f0, pos0, mlo, mhi, cnt, ent);
-    __builtin_amdgcn_sched_barrier(0);
-    f0 = fp;
-    if (roll_gather(gb, fp, ga, &d[2], tab, laneoff, mlo, mhi) == 0) [[unlikely]]
-        record16g(gb, f0, pos0 + 16, mlo, mhi, cnt, ent);
-    __builtin_amdgcn_sched_barrier(0);
-    f0 = fp;
-    if (roll_gather(ga, fp, gb, &d[3], tab, laneoff, mlo, mhi) == 0) [[unlikely]]
-        record16g(ga, f0, pos0 + 32, mlo, mhi, cnt, ent);
-    __builtin_amdgcn_sched_barrier(0);
-    f0 = fp;
-    if (roll_gather(gb, fp, ga, nullptr, tab, laneoff, mlo, mhi) == 0) [[unlikely]]
-        record16g(gb, f0, pos0 + 48, mlo, mhi, cnt, ent);
-#else
-    gather16(ga, d[0], tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    gather16(gb, d[1], tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    uint64_t f0 = fp;
-    if (roll16g(ga, fp, mlo, mhi) == 0) [[unlikely]] record16g(ga, f0, pos0, mlo, mhi, cnt, ent);
-    __builtin_amdgcn_sched_barrier(0);
-    gather16(ga, d[2], tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    f0 = fp;
-    if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 16, mlo, mhi, cnt, ent);
-    __builtin_amdgcn_sched_barrier(0);
-    gather16(gb, d[3], tab, laneoff);
-    __builtin_amdgcn_sched_barrier(0);
-    f0 = fp;
-    if (roll16g(ga, fp, mlo, mhi) == 0) [[unlikely]] record16g(ga, f0, pos0 + 32, mlo, mhi, cnt, ent);
-    __builtin_amdgcn_sched_barrier(0);
-    f0 = fp;
-    if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 48, mlo, mhi, cnt, ent);
-#endif
-}
-
-// One interior stage of G 16-byte groups (all positions tested), gathers one group ahead.
-template <int G>
-__device__ __forceinline__ void fast_stage_g(const uint4 (&d)[G], uint64_t &fp, uint64_t pos0,
-                                             const char *tab, uint32_t laneoff, uint32_t mlo,
-                                             uint32_t mhi, uint32_t *cnt, uint16_t *ent)
-{
-    if constexpr (G == 4) {
-        fast_stage(d, fp, pos0, tab, laneoff, mlo, mhi, cnt, ent);
-    } else {
-        static_assert(G == 2, "groups per stage");
-        uint64_t ga[16], gb[16];
-        gather16(ga, d[0], tab, laneoff);
-        __builtin_amdgcn_sched_barrier(0);
-        gather16(gb, d[1], tab, laneoff);
-        __builtin_amdgcn_sched_barrier(0);
-        uint64_t f0 = fp;
-        if (roll16g(ga, fp, mlo, mhi) == 0) [[unlikely]] record16g(ga, f0, pos0, mlo, mhi, cnt, ent);
-        __builtin_amdgcn_sched_barrier(0);
-        f0 = fp;
-        if (roll16g(gb, fp, mlo, mhi) == 0) [[unlikely]] record16g(gb, f0, pos0 + 16, mlo, mhi, cnt, ent);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -419,6 +238,7 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 #ifndef CDC_SCAN_STAGE
 #define CDC_SCAN_STAGE 64
 #endif
+
 constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
 constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
 constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane per stage = DMAs per stage
@@ -875,7 +695,7 @@ __device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64
     const uint32_t j = C.lane;
     const uint64_t pos = fz + j;
     const bool valid = (j + 1 < P.win) && pos < lim;
-    uint64_t v = valid ? lds_gear(C.tab, (byte << 8) | C.laneoff) : 0ull;
+    uint64_t v = valid ? lds_gear(C.tab, (byte << kWEntShift) | C.laneoff) : 0ull;
     v += dpp_shr64_zero<1>(v) << 1;
     v += dpp_shr64_zero<2>(v) << 2;
     v += dpp_shr64_zero<4>(v) << 4;
@@ -1033,21 +853,22 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
     C.tab = tab;
     C.lane = threadIdx.x & 63u;
-    C.laneoff = (C.lane & 31u) << 3;
+    C.laneoff = (C.lane & (kWCopies - 1u)) << 3;
     return C;
 }
 
 // ---------------------------------------------------------------------------
 // k_walk1: speculative chain per segment, started at the segment start.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, const DevParams P,
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(const Batch B, const DevParams P,
                                                                const Workspace W)
 {
-    __shared__ uint64_t s_tab[256 * 32];
+    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __shared__ uint64_t s_tab[256 * kWCopies];
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     const bool l0 = (threadIdx.x & 63u) == 0;
     if (l0) dbg_ts(B, kTsW1 + 8 * g);
-    fill_gear_lds<kWalkWavesPerWG * 64>(s_tab, W.gear);
+    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
     __syncthreads();
     if (l0) dbg_ts(B, kTsW1 + 8 * g + 1);
     if (g >= B.total_segs) return;
@@ -1094,14 +915,15 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk1(const Batch B, c
 // k_walk2: junction walk from the previous segment's exit until the chain
 // meets a node of some segment's speculative chain.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, const DevParams P,
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk2(const Batch B, const DevParams P,
                                                                const Workspace W)
 {
-    __shared__ uint64_t s_tab[256 * 32];
+    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __shared__ uint64_t s_tab[256 * kWCopies];
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     const bool l0 = (threadIdx.x & 63u) == 0;
     if (l0) dbg_ts(B, kTsW2 + 8 * g);
-    fill_gear_lds<kWalkWavesPerWG * 64>(s_tab, W.gear);
+    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
     __syncthreads();
     if (l0) dbg_ts(B, kTsW2 + 8 * g + 1);
     if (g >= B.total_segs) return;
@@ -1188,12 +1010,13 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_walk2(const Batch B, c
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSeqThreads = 256;
 
-__global__ __launch_bounds__(kSeqThreads) void k_seq(const Batch B, const DevParams P, const Workspace W)
+__global__ __launch_bounds__(kSeqThreads) CDC_WALK_ATTR void k_seq(const Batch B, const DevParams P, const Workspace W)
 {
-    __shared__ uint64_t s_tab[256 * 32];
+    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __shared__ uint64_t s_tab[256 * kWCopies];
     const uint32_t b = blockIdx.x;
     if (!B.force_fallback && W.flags[b] == 0) return;
-    fill_gear_lds<kSeqThreads>(s_tab, W.gear);
+    fill_gear_lds<kSeqThreads, kWCopies>(s_tab, W.gear);
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const BufDesc &D = B.b[b];
@@ -1245,7 +1068,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum
     return off + incl - v;
 }
 
-constexpr uint32_t kEmitThreads = 1024;
+constexpr uint32_t kEmitThreads = 512;  // 2 waves per SIMD: fits beside a scan workgroup
 constexpr uint32_t kEmitSlice = 64;     // segments written per emit workgroup
 constexpr uint32_t kEmitMaxWG = 64;     // emit workgroups per buffer
 
@@ -1261,9 +1084,12 @@ __host__ __device__ inline uint32_t emit_wgs(uint32_t nseg)
 // one wave per segment with lane i writing cut i (coalesced).
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const Batch B, const DevParams P, const Workspace W)
 {
-    __shared__ uint32_t s_nt[kNtCap];
-    __shared__ uint32_t s_ntc[kNtCap];  // merge segment of each listed junction
-    __shared__ uint32_t s_ivs[kNtCap], s_ive[kNtCap];
+    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    // u16 lists (segment indices < kMaxSegs; kConv* sentinels kept in the top
+    // three codes) so that an emit workgroup fits beside a scan workgroup.
+    __shared__ uint16_t s_nt[kNtCap];
+    __shared__ uint16_t s_ntc[kNtCap];  // merge segment of each listed junction
+    __shared__ uint16_t s_ivs[kNtCap], s_ive[kNtCap];
     __shared__ uint32_t s_off[kEmitSlice * 16];  // output index of the slice's segments (~0: invalid)
     __shared__ uint32_t s_wsum[16];
     __shared__ uint32_t s_m, s_niv, s_fail;
@@ -1313,8 +1139,8 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Batch B, const DevP
             const uint32_t pre = block_excl_scan(nt ? 1u : 0u, s_wsum, tot);
             const uint32_t m0 = s_m;
             if (nt && m0 + pre < kNtCap) {
-                s_nt[m0 + pre] = q;
-                s_ntc[m0 + pre] = c;
+                s_nt[m0 + pre] = uint16_t(q);
+                s_ntc[m0 + pre] = uint16_t(c >= kConvOvf ? c - 0xFFFF0000u : c);
             }
             __syncthreads();
             if (tid == 0) s_m = m0 + tot;
@@ -1332,15 +1158,16 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit(const Batch B, const DevP
             for (uint32_t i = 0; i < m; ++i) {
                 const uint32_t p = s_nt[i];
                 if (p < cur) continue;  // skipped by an earlier junction walk
-                const uint32_t c = s_ntc[i];
+                const uint32_t c16 = s_ntc[i];
+                const uint32_t c = c16 >= (kConvOvf & 0xFFFFu) ? c16 + 0xFFFF0000u : c16;
                 if (c == kConvOvf) {
                     fail = 1;
                     break;
                 }
                 const uint32_t j = c >= kConvOvf ? NS : c + 1;
                 if (j > p + 1) {
-                    s_ivs[niv] = p + 1;
-                    s_ive[niv] = j;
+                    s_ivs[niv] = uint16_t(p + 1);
+                    s_ive[niv] = uint16_t(j);  // j <= NS <= kMaxSegs
                     ++niv;
                 }
                 cur = j;

@@ -198,6 +198,25 @@ def test_batch_many_buffers(oracle):
         assert_same(got[i], oracle.chunk(a, gear, **p), f"buffer {i} ({a.size} B)")
 
 
+def test_pipelined_streams(oracle):
+    """Two batches over the same buffers alternate over two streams (bench.py's
+    pipelined steps): one batch's resolution kernels run beside the next
+    batch's scan; every pass must still produce the oracle's cut lists."""
+    arrays = [random_bytes(24 << 20, 71), random_bytes((5 << 20) + 123, 72), low_entropy(9 << 20, 73)]
+    gear = _placeholder()
+    _lib.ensure_init(gear=gear)
+    ts = [torch.from_numpy(a).cuda() for a in arrays]
+    batches = [device.DeviceBatch(ts, _opts(DEF)) for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    for i in range(6):
+        batches[i % 2].launch(streams[i % 2])
+    refs = [oracle.chunk(a, gear, **DEF) for a in arrays]
+    for k, b in enumerate(batches):
+        cuts, _ = b.results()
+        for i, (c, r) in enumerate(zip(cuts, refs)):
+            assert_same(c.cpu().numpy().astype(np.uint64), r, f"stream {k} buffer {i}")
+
+
 def test_c2_shape_32x64MiB(oracle):
     """BASELINE configs[2], one GPU's share: 32 x 64 MiB random buffers."""
     arrays = [random_bytes(64 << 20, 100 + i) for i in range(32)]
