@@ -835,6 +835,174 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
     return clipped ? kUndet : p + n;
 }
 
+// ---------------------------------------------------------------------------
+// Speculative walking.  On ordinary data next(p) is "the first full-window
+// MaskS candidate in [p + Min + W - 1, p + Normal)" + cut_adj: a hit in the
+// truncated window (the W - 1 positions after p + Min, fingerprint reset
+// there) has probability ~(W - 1) 2^-15 per node.  So a walk
+//   1. preloads the candidate-index blocks it can reach into wave-local LDS
+//      (one global round trip),
+//   2. follows candidate-only successors through LDS for up to kSpecK nodes,
+//   3. loads the truncated-window bytes of all those nodes at once (one round
+//      trip) and verifies them in order: the first node whose truncated window
+//      hits takes that hit as its successor, and the next round starts there.
+// A step the preload cannot answer (a dense index block, a reach beyond the
+// preloaded blocks, the MaskL region, the last Min bytes of the buffer) takes
+// the exact next_node().  Results are identical to next_node() step by step.
+// ---------------------------------------------------------------------------
+#ifndef CDC_WALK_SPEC
+#define CDC_WALK_SPEC 0
+#endif
+constexpr uint32_t kSpecK = 16;     // nodes speculated per round
+constexpr uint32_t kPreBlk = 128;   // index blocks preloaded per wave (8.5 KiB of LDS)
+static constexpr uint64_t kSpecMiss = ~1ull;
+
+struct SpecIdx {
+    uint32_t *cnt;  // LDS [kPreBlk]
+    uint16_t *ent;  // LDS [kPreBlk * kIdxCap], 16-B aligned
+    uint64_t b0;    // first preloaded block
+    uint32_t nb;    // preloaded blocks, all sparse (0: none)
+};
+
+// Preload blocks [b0, b1] (clipped to the buffer and to kPreBlk), up to the
+// first dense one.
+__device__ void spec_preload(const WalkCtx &C, SpecIdx &S, uint64_t b0, uint64_t b1)
+{
+    const uint64_t nblk = (C.len + kIdxBlock - 1) >> kIdxShift;
+    S.b0 = b0;
+    S.nb = 0;
+    if (nblk == 0 || b0 >= nblk) return;
+    if (b1 >= nblk) b1 = nblk - 1;
+    if (b1 < b0) return;
+    const uint32_t nb = uint32_t(min<uint64_t>(b1 - b0 + 1, kPreBlk));
+    uint32_t first_dense = 0xFFFFFFFFu;
+    for (uint32_t i = C.lane; i < nb; i += 64) {
+        const uint32_t c = C.cnt[b0 + i];
+        S.cnt[i] = c;
+        if (c > kIdxCap && i < first_dense) first_dense = i;
+    }
+    const uint4 *src = reinterpret_cast<const uint4 *>(C.ent + b0 * kIdxCap);
+    uint4 *dst = reinterpret_cast<uint4 *>(S.ent);
+    for (uint32_t i = C.lane; i < nb * (kIdxCap * 2 / 16); i += 64) dst[i] = src[i];
+    S.nb = min(nb, wave_min_u32(first_dense));
+}
+
+// First candidate in [a, b) from the preload; kNoHit if there is none,
+// kSpecMiss if the preload cannot tell.  Lanes 0-31 / 32-63 read the slots of
+// two consecutive blocks per iteration.
+__device__ uint64_t spec_first(const WalkCtx &C, const SpecIdx &S, uint64_t a, uint64_t b)
+{
+    const uint64_t bl = (b - 1) >> kIdxShift;
+    for (uint64_t blk = a >> kIdxShift; blk <= bl; blk += 2) {
+        if (blk < S.b0) return kSpecMiss;
+        const uint64_t bi = blk + (C.lane >> 5);
+        const uint64_t li = bi - S.b0;
+        const bool want = bi <= bl;
+        if (__ballot(want && li >= S.nb)) return kSpecMiss;
+        uint32_t rel = 0xFFFFFFFFu;
+        const uint32_t slot = C.lane & 31u;
+        if (want && slot < S.cnt[li]) {
+            const uint64_t pos = (bi << kIdxShift) + S.ent[li * kIdxCap + slot];
+            if (pos >= a && pos < b) rel = uint32_t(pos - a);
+        }
+        rel = wave_min_u32(rel);
+        if (rel != 0xFFFFFFFFu) return a + rel;
+    }
+    return kNoHit;
+}
+
+// The chunk window next_node() works on for a chunk starting at p (r > Min).
+struct ChunkWin {
+    uint64_t fz, norm_end, lim;
+};
+
+__device__ __forceinline__ ChunkWin chunk_win(const WalkCtx &C, const DevParams &P, uint64_t p)
+{
+    const uint64_t r = C.len - p;
+    uint64_t norm = P.normal_size, lim;
+    if (C.final_) {
+        uint64_t n;
+        if (r >= P.max_size) {
+            n = P.max_size;
+        } else {
+            n = r;
+            if (r <= P.normal_size) norm = r;
+        }
+        lim = p + n;
+    } else {
+        lim = min(p + P.max_size, C.len);
+    }
+    return ChunkWin{p + P.min_size, p + norm, lim};
+}
+
+// Candidate-only successor of x (its truncated window still to verify), or
+// kSpecMiss when the preload cannot answer (the caller then takes next_node).
+__device__ __forceinline__ uint64_t spec_cand(const WalkCtx &C, const DevParams &P, const SpecIdx &S, uint64_t x)
+{
+    if (C.len - x <= P.min_size) return kSpecMiss;
+    const ChunkWin w = chunk_win(C, P, x);
+    const uint64_t full0 = w.fz + (P.win - 1);
+    const uint64_t s_end = min(w.norm_end, w.lim);
+    if (full0 >= s_end) return kSpecMiss;
+    const uint64_t q = spec_first(C, S, full0, s_end);
+    return (q == kNoHit || q == kSpecMiss) ? kSpecMiss : q + P.cut_adj;
+}
+
+// Wave-local LDS scratch of one speculative round.
+struct SpecBuf {
+    uint64_t x[kSpecK];    // node
+    uint64_t nx[kSpecK];   // its successor
+    uint32_t ex[kSpecK];   // 1: nx is next_node()'s (exact), 0: candidate-only
+    uint8_t byt[kSpecK][64];
+    uint64_t t_spec;       // debug: s_memrealtime after the speculation loop
+};
+
+// One speculative round from x: up to kSpecK verified successors in R.nx[0..n),
+// stopping after the first one that is kUndet, >= len or >= stop.  Returns n.
+__device__ uint32_t spec_round(const WalkCtx &C, const DevParams &P, const SpecIdx &S, uint64_t x, uint64_t stop,
+                               SpecBuf &R)
+{
+    uint32_t n = 0;
+    for (uint64_t y = x; n < kSpecK;) {
+        uint64_t q = spec_cand(C, P, S, y);
+        const bool exact = q == kSpecMiss;
+        if (exact) q = next_node(C, P, y);
+        if (C.lane == 0) {
+            R.x[n] = y;
+            R.nx[n] = q;
+            R.ex[n] = exact ? 1u : 0u;
+        }
+        ++n;
+        if (q == kUndet || q >= C.len || q >= stop) break;
+        y = q;
+    }
+    if (C.lane == 0) R.t_spec = __builtin_amdgcn_s_memrealtime();
+    // the truncated-window bytes of every speculated node, in one round trip
+    const uint8_t *data = reinterpret_cast<const uint8_t *>(C.ub);
+    uint32_t byt[kSpecK];
+#pragma unroll
+    for (uint32_t k = 0; k < kSpecK; ++k) {
+        byt[k] = 0;
+        if (k < n && !R.ex[k]) {
+            const ChunkWin w = chunk_win(C, P, R.x[k]);
+            const uint64_t pos = w.fz + C.lane;
+            if (C.lane + 1 < P.win && pos < w.lim) byt[k] = data[pos];
+        }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSpecK; ++k) R.byt[k][C.lane] = uint8_t(byt[k]);
+    for (uint32_t k = 0; k < n; ++k) {
+        if (R.ex[k]) continue;
+        const ChunkWin w = chunk_win(C, P, R.x[k]);
+        const uint64_t h = trunc_first_hit(C, P, w.fz, w.norm_end, w.lim, R.byt[k][C.lane]);
+        if (h != kNoHit) {
+            if (C.lane == 0) R.nx[k] = h + P.cut_adj;
+            return k + 1;
+        }
+    }
+    return n;
+}
+
 __device__ __forceinline__ uint32_t buf_of_seg(const Batch &B, uint32_t g)
 {
     uint32_t b = 0;
@@ -865,6 +1033,11 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
 {
     __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
+#if CDC_WALK_SPEC
+    __shared__ uint32_t s_pcnt[kWalkWavesPerWG][kPreBlk];
+    __shared__ __attribute__((aligned(16))) uint16_t s_pent[kWalkWavesPerWG][kPreBlk * kIdxCap];
+    __shared__ SpecBuf s_spec[kWalkWavesPerWG];
+#endif
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     const bool l0 = (threadIdx.x & 63u) == 0;
     if (l0) dbg_ts(B, kTsW1 + 8 * g);
@@ -882,17 +1055,41 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
     uint32_t c = 0;
     if (C.lane == 0) nodes[c] = p;
     ++c;
-    uint64_t nx;
+    uint64_t nx = p;
+#if CDC_WALK_SPEC
+    SpecIdx S;
+    S.cnt = s_pcnt[threadIdx.x >> 6];
+    S.ent = s_pent[threadIdx.x >> 6];
+    spec_preload(C, S, (p + P.min_size) >> kIdxShift, (seg_end + P.max_size) >> kIdxShift);
+    if (C.lane == 0) dbg_ts(B, kTsW1 + 8 * g + 2);
+    SpecBuf &R = s_spec[threadIdx.x >> 6];
+    for (uint32_t round = 0, done = 0; !done; ++round) {
+        const uint32_t n = spec_round(C, P, S, p, seg_end, R);
+        if (C.lane == 0 && round == 0) {
+            dbg_ts(B, kTsW1 + 8 * g + 5, __builtin_amdgcn_s_memrealtime());
+            dbg_ts(B, kTsW1 + 8 * g + 7, R.t_spec);
+        }
+        if (C.lane == 0) dbg_ts(B, kTsW1 + 8 * g + 6, round + 1);
+        for (uint32_t k = 0; k < n; ++k) {
+            nx = R.nx[k];
+            if (C.lane == 0) nodes[c] = nx;
+            ++c;
+            if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) {
+                done = 1;
+                break;
+            }
+        }
+        p = nx;
+    }
+#else
     for (;;) {
         nx = next_node(C, P, p);
-        if (C.lane == 0) {
-            nodes[c] = nx;
-            if (c == 1) dbg_ts(B, kTsW1 + 8 * g + 2);
-        }
+        if (C.lane == 0) nodes[c] = nx;
         ++c;
         if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) break;
         p = nx;
     }
+#endif
     if (C.lane == 0) {
         W.w1_cnt[g] = c;
         W.w1_exit[g] = nx;

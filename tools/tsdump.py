@@ -70,7 +70,10 @@ def main():
     w2 = ts[K_W2:K_EMIT].reshape(-1, 8)[:nseg]
     print(f"walk1 segs {nseg}: start {pct(us(w1[:, 0]))}")
     print(f"  fill done {pct(us(w1[:, 1]))}")
-    print(f"  1st node  {pct(us(w1[:, 2]))}")
+    print(f"  1st node / preload done {pct(us(w1[:, 2]))}")
+    if w1[:, 5].max() > 0:
+        print(f"  1st spec loop done  {pct(us(w1[:, 7]))}")
+        print(f"  1st spec round done {pct(us(w1[:, 5]))}   rounds {pct(w1[:, 6])}")
     print(f"  end       {pct(us(w1[:, 3]))}")
     print(f"  per-wave (end - fill) {pct((w1[:, 3] - w1[:, 1]) / 100.0)}  nodes {pct(w1[:, 4])}")
     ok = w2[:, 3] > 0
