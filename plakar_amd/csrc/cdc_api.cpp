@@ -208,8 +208,7 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
 {
     char *b = static_cast<char *>(ws);
     Workspace W;
-    W.blk_cnt = reinterpret_cast<uint32_t *>(b + pl.off_blk_cnt);
-    W.blk_ent = reinterpret_cast<uint16_t *>(b + pl.off_blk_ent);
+    W.runs = reinterpret_cast<uint64_t *>(b + pl.off_runs);
     W.w1_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w1_nodes);
     W.w1_cnt = reinterpret_cast<uint32_t *>(b + pl.off_w1_cnt);
     W.w2_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w2_nodes);
@@ -234,7 +233,6 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     B.nbufs = uint32_t(n);
     B.final_ = final_ ? 1u : 0u;
     B.total_segs = pl.total_segs;
-    B.total_blks = pl.total_blks;
     B.total_tasks = pl.total_tasks;
     B.cap1 = pl.cap1;
     B.cap2 = pl.cap2;
@@ -246,7 +244,7 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     }();
     B.debug = dbg;
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
-    uint32_t segs = 0, blks = 0, tasks = 0;
+    uint32_t segs = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
         BufDesc &D = B.b[i];
         D.data = static_cast<const uint8_t *>(data[i]);
@@ -256,10 +254,8 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         D.res = res[i];
         D.seg_base = segs;
         D.nseg = uint32_t((lens[i] + pl.seg - 1) / pl.seg);
-        D.blk_base = blks;
         D.task_base = tasks;
         segs += D.nseg;
-        blks += uint32_t((lens[i] + kIdxBlock - 1) / kIdxBlock);
         tasks += uint32_t(align_tasks((lens[i] + 64ull * pl.scan_lane - 1) / (64ull * pl.scan_lane)));
     }
     const Workspace W = carve(ws, pl, ctx->d_gear);

@@ -10,11 +10,17 @@
 namespace cdc {
 
 constexpr int kMaxBufsPerLaunch = 32;   // buffers per launch group (kernel-arg budget)
-constexpr uint32_t kIdxShift = 16;      // candidate-index block = 64 KiB of input
-constexpr uint64_t kIdxBlock = 1ull << kIdxShift;
-constexpr uint32_t kIdxCap = 32;        // u16 entries per index block (one 64-B line)
+// Candidate index: one u64 record per scan-lane run (scan_lane bytes of one
+// buffer): bits 0-15 the number of full-window MaskS candidates in the run
+// (saturating), bits 16-63 the first kRunCap of them as u16 offsets from the
+// run start, ascending.  Written once per run by the lane that scanned it (no
+// atomics, no zeroing); runs and their entries are in position order, so the
+// index is sorted by construction.  A run with more than kRunCap candidates is
+// "dense": walkers rescan its bytes.
+constexpr uint32_t kRunCap = 3;
+constexpr uint32_t kMaxScanLane = 65536;  // run offsets are u16
 constexpr uint32_t kMaxSegs = 16384;    // resolution segments per buffer
-constexpr uint32_t kScanLaneBytes = 8192;  // max bytes hashed+tested per scan lane (multiple of 128)
+constexpr uint32_t kScanLaneBytes = 16384;  // max bytes hashed+tested per scan lane (multiple of 256)
 constexpr uint32_t kWalkWavesPerWG = 4;   // latency-bound walkers: registers over occupancy
 constexpr uint64_t kUndet = ~0ull;      // "next chunk start not decided by the bytes present"
 
@@ -37,17 +43,16 @@ struct BufDesc {
     cdc_result *res;
     uint32_t seg_base;   // first resolution segment (global numbering)
     uint32_t nseg;
-    uint32_t blk_base;   // first candidate-index block (global numbering)
     uint32_t task_base;  // first scan task (global numbering)
 };
 
 struct Batch {
     uint32_t nbufs;
     uint32_t final_;
-    uint32_t total_segs, total_blks, total_tasks;
+    uint32_t total_segs, total_tasks;
     uint32_t cap1, cap2;     // per-segment node capacities (speculative / junction walks)
     uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
-    uint32_t scan_lane;      // bytes per scan lane; one wave (scan task) = 64 lanes
+    uint32_t scan_lane;      // bytes per scan lane (= per index run); one wave (scan task) = 64 lanes
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];
@@ -68,8 +73,7 @@ struct Piece {
 
 // Device workspace, carved out of one caller-provided allocation.
 struct Workspace {
-    uint32_t *blk_cnt;   // [total_blks] candidates seen per index block
-    uint16_t *blk_ent;   // [total_blks * kIdxCap] offsets inside the block
+    uint64_t *runs;      // [total_tasks * 64] candidate-index records (run q of buffer b at 64 * task_base + q)
     uint64_t *w1_nodes;  // [total_segs * cap1] speculative chain per segment
     uint32_t *w1_cnt;    // [total_segs]
     uint64_t *w2_nodes;  // [total_segs * cap2] junction walk per segment
@@ -87,14 +91,14 @@ struct Plan {
     uint64_t seg;
     uint32_t scan_lane;
     uint32_t cap1, cap2;
-    uint32_t total_segs, total_blks, total_tasks;
-    size_t off_blk_cnt, off_blk_ent, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_piece, off_flags,
+    uint32_t total_segs, total_tasks;
+    size_t off_runs, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_piece, off_flags,
         off_w1_exit, bytes;
 };
 
 // Host-side helpers implemented in cdc_kernels.hip.
 // Scan tasks of one buffer, rounded up so that every buffer starts on a scan
-// workgroup boundary (k_scan zeroes the index blocks it owns).
+// workgroup boundary (one buffer per workgroup: uniform stage alignment).
 uint64_t align_tasks(uint64_t tasks);
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan);
 int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream);

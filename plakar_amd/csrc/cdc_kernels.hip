@@ -155,16 +155,6 @@ __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp
     return hit;
 }
 
-// ---------------------------------------------------------------------------
-// Scan helpers: full-window MaskS candidates of every byte into the index.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void index_append(uint32_t *cnt, uint16_t *ent, uint64_t pos)
-{
-    const uint64_t blk = pos >> kIdxShift;
-    const uint32_t slot = atomicAdd(&cnt[blk], 1u);
-    if (slot < kIdxCap) ent[blk * kIdxCap + slot] = uint16_t(pos & (kIdxBlock - 1));
-}
-
 __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
 {
     uint32_t r;
@@ -250,13 +240,10 @@ constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
 static_assert(kNBuf >= 1 && kNBuf <= 3, "ring depth");
 static_assert(kGearLdsBytes + kS2Waves * kNBuf * kStageBytes <= 160u * 1024u, "LDS budget");
-// Scan lane lengths are multiples of kLaneQuant, so that one workgroup covers
-// whole 64-KiB index blocks (k_scan zeroes the blocks it owns).
-constexpr uint32_t lane_quant(uint32_t q)
-{
-    return (kS2Waves * 64u * q) % 65536u == 0 ? q : lane_quant(2 * q);
-}
-constexpr uint32_t kLaneQuant = lane_quant(128);
+// Scan lane lengths are multiples of kLaneQuant (16-B aligned runs: every lane
+// of a buffer has the same stage alignment; 256 B avoided the slow strides
+// seen at odd multiples of 128 B, see make_plan).
+constexpr uint32_t kLaneQuant = 256;
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
@@ -327,28 +314,17 @@ __device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uin
     }
 }
 
-// Hits found by the scan are held in two per-lane registers and appended to
-// the candidate index after the lane's last stage: a returning global atomic
-// waits (vmcnt) for every older vector-memory operation, i.e. for the stages
-// in flight, so appends inside the loop would drain the DMA pipeline.  A third
-// hit in one lane run (rare on random data; every byte on degenerate data)
-// is appended at once.
-struct PendingHits {
-    uint64_t slots = 0;  // up to two u32 run-relative positions
-    uint32_t n = 0;
-};
-
-__device__ __forceinline__ void record_hit(PendingHits &ph, int32_t r, int64_t s, uint32_t *cnt, uint16_t *ent)
+// Each lane keeps its run's index record in a register (count + the first
+// kRunCap offsets, see cdc_internal.h) and stores it after its last stage:
+// one coalesced 8-byte store per run, no atomics.
+__device__ __forceinline__ void record_hit(uint64_t &rec, int32_t r)
 {
 #if CDC_DIAG_NO_APPEND
     if (r != 0x7FFFFFF0) return;
 #endif
-    if (ph.n < 2) {
-        ph.slots |= uint64_t(uint32_t(r)) << (32 * ph.n);
-        ++ph.n;
-    } else {
-        index_append(cnt, ent, uint64_t(s + r));
-    }
+    const uint32_t c = uint32_t(rec & 0xFFFFu);
+    if (c < kRunCap) rec |= uint64_t(uint32_t(r)) << (16u + 16u * c);
+    if (c < 0xFFFFu) ++rec;
 }
 
 // Exact MaskS test of one 16-byte group in the shifted frame, from fp' before
@@ -358,8 +334,7 @@ __device__ __forceinline__ void record_hit(PendingHits &ph, int32_t r, int64_t s
 // hi-dword filter fired in some lane of the wave (2^-13 per byte at the
 // default masks), exec-masked to those lanes.
 __device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16], int32_t r0, int32_t len,
-                                           uint32_t xlo, uint32_t xhi, PendingHits &ph, int64_t s, uint32_t *cnt,
-                                           uint16_t *ent)
+                                           uint32_t xlo, uint32_t xhi, uint64_t &rec)
 {
     uint32_t key[16];
     uint32_t m = 0xFFFFFFFFu;
@@ -374,33 +349,13 @@ __device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int32_t r = r0 + k;
-        if (key[k] == 0 && r >= 0 && r < len) record_hit(ph, r, s, cnt, ent);
+        if (key[k] == 0 && r >= 0 && r < len) record_hit(rec, r);
     }
 }
 
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
 {
     __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kNBuf * kStageBytes];
-    // Zero this workgroup's candidate-index counts.  Every buffer's tasks start
-    // on a workgroup boundary and a workgroup covers kS2Waves * 64 * scan_lane
-    // bytes (a multiple of the 64-KiB index block), so no other workgroup
-    // touches these blocks: the barrier below orders the zeroing before every
-    // append, and no separate memset launch is needed.
-    {
-        const uint32_t tw = blockIdx.x * kS2Waves + (threadIdx.x >> 6);
-        if (tw < B.total_tasks) {
-            uint32_t bw = 0;
-            while (bw + 1 < B.nbufs && tw >= B.b[bw + 1].task_base) ++bw;
-            const BufDesc &Dw = B.b[bw];
-            const uint64_t lo = uint64_t(tw - Dw.task_base) * 64u * B.scan_lane;
-            if (lo < Dw.len) {
-                const uint64_t hi = min(lo + 64ull * B.scan_lane, Dw.len);
-                uint32_t *cz = W.blk_cnt + Dw.blk_base;
-                for (uint64_t k = (lo >> kIdxShift) + (threadIdx.x & 63u); k < ((hi + kIdxBlock - 1) >> kIdxShift); k += 64)
-                    cz[k] = 0;
-            }
-        }
-    }
     if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, P.fs_sh);
     __syncthreads();
@@ -450,8 +405,6 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     auto slot_of = [&](uint32_t t) -> const char * {
         return s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + lane * kStage;
     };
-    uint32_t *cnt = W.blk_cnt + D.blk_base;
-    uint16_t *ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
     const uint32_t vhi = to_vgpr(P.fs_hi);
     const uint32_t xlo = P.fs_lo, xhi = P.fs_hi;
     const uint32_t swz = stage_swz(lane);
@@ -479,7 +432,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
 #pragma unroll
     for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
     uint64_t fp = 0;
-    PendingHits ph;
+    uint64_t rec = 0;  // this lane's run record
     const int32_t len = int32_t(e - s);
     const int32_t rr0 = int32_t(rel0 - s);  // run-relative position of the lane's first staged byte
     for (uint32_t t = 0; t < T; ++t) {
@@ -506,7 +459,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
             uint64_t (&nxt)[16] = gv[(gi + 1) & 1];
 #if CDC_DIAG_NO_COMPUTE
             fp += nx.x ^ d[gi].w;  // diagnostic: staging only
-            if (fp == 0x123456789ull) index_append(cnt, ent, 0);
+            if (fp == 0x123456789ull) rec = fp;
             continue;
 #endif
             const uint64_t f0 = fp;
@@ -530,13 +483,12 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
 #else
             if (acc == 0) [[unlikely]]
 #endif
-                recheck_group(f0, cur, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, ph, s, cnt, ent);
+                recheck_group(f0, cur, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
         }
 #pragma unroll
         for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
     }
-    // the pending hits (up to two per lane)
-    for (uint32_t k = 0; k < ph.n; ++k) index_append(cnt, ent, uint64_t(s + int32_t(uint32_t(ph.slots >> (32 * k)))));
+    if (s < int64_t(D.len)) W.runs[64ull * D.task_base + seg0 + lane] = rec;
     if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
 
@@ -637,8 +589,9 @@ struct WalkCtx {
     uint64_t ub;       // absolute address of byte 0
     uint64_t len;
     uint32_t final_;
-    const uint32_t *cnt;
-    const uint16_t *ent;
+    const uint64_t *runs;  // this buffer's index records (run q at runs[q])
+    uint64_t sl;           // run length (scan lane bytes)
+    double inv_sl;
     const char *tab;
     uint32_t laneoff;
     uint32_t lane;
@@ -714,38 +667,66 @@ __device__ uint64_t trunc_first_hit(const WalkCtx &C, const DevParams &P, uint64
     return m ? fz + uint64_t(__ffsll((unsigned long long)m) - 1) : kNoHit;
 }
 
-// First full-window MaskS candidate in [a, b), from the index.  Index blocks
-// that overflowed (dense data) are rescanned raw.
-__device__ __noinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
-                                    uint64_t fz)
+// Index run holding position x.
+__device__ __forceinline__ uint64_t run_of(const WalkCtx &C, uint64_t x)
 {
-    const uint64_t blk0 = a >> kIdxShift, blk1 = (b - 1) >> kIdxShift;
-    for (uint64_t base = blk0; base <= blk1; base += 64) {
-        const uint64_t blk = base + C.lane;
-        const bool in = blk <= blk1;
-        const uint32_t c = in ? C.cnt[blk] : 0u;
-        const bool dense = in && c > kIdxCap;
-        uint64_t best = kNoHit;
-        if (in && !dense) {
-            const uint64_t bstart = blk << kIdxShift;
-            const uint16_t *e = C.ent + blk * kIdxCap;
-            for (uint32_t i = 0; i < c; ++i) {
-                const uint64_t pos = bstart + e[i];
-                if (pos >= a && pos < b && pos < best) best = pos;
-            }
-        }
-        uint64_t found = __ballot(best != kNoHit);
-        uint64_t dn = __ballot(dense);
-        while (found | dn) {
-            const int lf = found ? __ffsll((unsigned long long)found) - 1 : 64;
-            const int ld = dn ? __ffsll((unsigned long long)dn) - 1 : 64;
-            if (lf < ld) return readlane64(best, lf);
-            const uint64_t db = base + uint64_t(ld);
-            const uint64_t lo = max(a, db << kIdxShift), hi = min(b, (db + 1) << kIdxShift);
-            const uint64_t h = raw_first_hit(C, lo, hi, fz, P.ms_lo, P.ms_hi);
-            if (h != kNoHit) return h;
-            dn &= ~(1ull << ld);
-        }
+    uint64_t q = uint64_t(double(x) * C.inv_sl);
+    if (q * C.sl > x) --q;
+    else if ((q + 1) * C.sl <= x) ++q;
+    return q;
+}
+
+// First stored candidate of a run record (run start rs) in [a, b), or kNoHit.
+// Stored entries are the run's smallest kRunCap, ascending: the smallest one
+// >= a is the run's first candidate >= a even when the run is dense.
+__device__ __forceinline__ uint64_t rec_first(uint64_t rec, uint64_t rs, uint64_t a, uint64_t b)
+{
+    const uint32_t n = min(uint32_t(rec & 0xFFFFu), kRunCap);
+    uint64_t best = kNoHit;
+#pragma unroll
+    for (int i = int(kRunCap) - 1; i >= 0; --i) {
+        const uint64_t pos = rs + ((rec >> (16 + 16 * i)) & 0xFFFFu);
+        if (uint32_t(i) < n && pos >= a && pos < b) best = pos;
+    }
+    return best;
+}
+
+// Resolve a wave's 64 consecutive run records (run r0 + lane, valid lanes
+// `in`): the first candidate in [a, b), rescanning dense runs whose stored
+// entries do not answer.  *done = false when none of these runs holds one.
+__device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0, bool in, uint64_t rec, uint64_t a,
+                               uint64_t b, uint64_t fz, bool &done)
+{
+    const uint64_t rs = (r0 + C.lane) * C.sl;
+    const uint64_t cand = in ? rec_first(rec, rs, a, b) : kNoHit;
+    uint64_t mc = __ballot(cand != kNoHit);
+    uint64_t md = __ballot(in && cand == kNoHit && (rec & 0xFFFFu) > kRunCap);
+    done = true;
+    while (mc | md) {
+        const int lf = mc ? __ffsll((unsigned long long)mc) - 1 : 64;
+        const int ld = md ? __ffsll((unsigned long long)md) - 1 : 64;
+        if (lf < ld) return readlane64(cand, lf);
+        const uint64_t rr = r0 + uint64_t(ld);
+        const uint64_t lo = max(a, rr * C.sl), hi = min(b, (rr + 1) * C.sl);
+        const uint64_t h = raw_first_hit(C, lo, hi, fz, P.ms_lo, P.ms_hi);
+        if (h != kNoHit) return h;
+        md &= ~(1ull << ld);
+    }
+    done = false;
+    return kNoHit;
+}
+
+// First full-window MaskS candidate in [a, b) from the run index.
+__device__ __noinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+                                                 uint64_t fz)
+{
+    const uint64_t rl = run_of(C, b - 1);
+    for (uint64_t r0 = run_of(C, a); r0 <= rl; r0 += 64) {
+        const bool in = r0 + C.lane <= rl;
+        const uint64_t rec = in ? C.runs[r0 + C.lane] : 0ull;
+        bool done;
+        const uint64_t h = recs_first(C, P, r0, in, rec, a, b, fz, done);
+        if (done) return h;
     }
     return kNoHit;
 }
@@ -787,42 +768,23 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
     // ---- fused loads
     const uint64_t tpos = fz + j;
     const bool tvalid = (j + 1 < P.win) && tpos < lim;
-    const uint64_t blk0 = full0 >> kIdxShift;
-    const uint64_t blk1 = has_s ? (s_end - 1) >> kIdxShift : 0;
-    const bool bin = has_s && blk0 + j <= blk1;
-    const uint64_t eblk = blk0 + (j >> 4);
-    const bool ein = has_s && j < 32 && eblk <= blk1;
-    uint32_t byte = 0, cnt = 0, epair = 0;
+    const uint64_t r0 = has_s ? run_of(C, full0) : 0;
+    const uint64_t rl = has_s ? run_of(C, s_end - 1) : 0;
+    const bool rin = has_s && r0 + j <= rl;
+    uint32_t byte = 0;
+    uint64_t rec = 0;
     if (tvalid) byte = reinterpret_cast<const uint8_t *>(C.ub)[tpos];
-    if (bin) cnt = C.cnt[blk0 + j];
-    if (ein) epair = *reinterpret_cast<const uint32_t *>(C.ent + eblk * kIdxCap + 2u * (j & 15u));
+    if (rin) rec = C.runs[r0 + j];
     // ---- truncated window [fz, fz + W - 1)
     uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim, byte);
     if (h != kNoHit) return h + P.cut_adj;
     // ---- full-window MaskS candidates in [full0, s_end)
     if (has_s) {
-        const uint32_t c0 = uint32_t(__builtin_amdgcn_readlane(cnt, 0));
-        const uint32_t c1 = uint32_t(__builtin_amdgcn_readlane(cnt, 1));
-        const bool two = blk0 + 1 <= blk1;
-        if (c0 <= kIdxCap && (!two || c1 <= kIdxCap)) {
-            const uint32_t ce = j < 16 ? c0 : c1;
-            const uint32_t i0 = 2u * (j & 15u);
-            const uint64_t bs = eblk << kIdxShift;
-            uint64_t best = kNoHit;
-            if (ein) {
-                const uint64_t q0 = bs + (epair & 0xFFFFu), q1 = bs + (epair >> 16);
-                if (i0 < ce && q0 >= full0 && q0 < s_end) best = q0;
-                if (i0 + 1 < ce && q1 >= full0 && q1 < s_end && q1 < best) best = q1;
-            }
-            // offsets from full0 fit in 32 bits (< MaxSize <= 1 GiB)
-            const uint32_t rel = wave_min_u32(best == kNoHit ? 0xFFFFFFFFu : uint32_t(best - full0));
-            if (rel != 0xFFFFFFFFu) return full0 + rel + P.cut_adj;
-            if (blk0 + 2 <= blk1) {
-                h = index_first_hit(C, P, (blk0 + 2) << kIdxShift, s_end, fz);
-                if (h != kNoHit) return h + P.cut_adj;
-            }
-        } else {
-            h = index_first_hit(C, P, full0, s_end, fz);
+        bool done;
+        h = recs_first(C, P, r0, rin, rec, full0, s_end, fz, done);
+        if (done) return h + P.cut_adj;
+        if (r0 + 64 <= rl) {
+            h = index_first_hit(C, P, (r0 + 64) * C.sl, s_end, fz);
             if (h != kNoHit) return h + P.cut_adj;
         }
     }
@@ -853,60 +815,48 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
 #ifndef CDC_WALK_SPEC
 #define CDC_WALK_SPEC 0
 #endif
-constexpr uint32_t kSpecK = 16;     // nodes speculated per round
-constexpr uint32_t kPreBlk = 128;   // index blocks preloaded per wave (8.5 KiB of LDS)
+constexpr uint32_t kSpecK = 16;      // nodes speculated per round
+constexpr uint32_t kPreRuns = 1024;  // index runs preloaded per wave (8 KiB of LDS)
 static constexpr uint64_t kSpecMiss = ~1ull;
 
 struct SpecIdx {
-    uint32_t *cnt;  // LDS [kPreBlk]
-    uint16_t *ent;  // LDS [kPreBlk * kIdxCap], 16-B aligned
-    uint64_t b0;    // first preloaded block
-    uint32_t nb;    // preloaded blocks, all sparse (0: none)
+    uint64_t *rec;  // LDS [kPreRuns]
+    uint64_t r0;    // first preloaded run
+    uint32_t nr;    // preloaded runs
 };
 
-// Preload blocks [b0, b1] (clipped to the buffer and to kPreBlk), up to the
-// first dense one.
-__device__ void spec_preload(const WalkCtx &C, SpecIdx &S, uint64_t b0, uint64_t b1)
+// Preload the run records covering [a, b) (clipped to the buffer and kPreRuns).
+__device__ void spec_preload(const WalkCtx &C, SpecIdx &S, uint64_t a, uint64_t b)
 {
-    const uint64_t nblk = (C.len + kIdxBlock - 1) >> kIdxShift;
-    S.b0 = b0;
-    S.nb = 0;
-    if (nblk == 0 || b0 >= nblk) return;
-    if (b1 >= nblk) b1 = nblk - 1;
-    if (b1 < b0) return;
-    const uint32_t nb = uint32_t(min<uint64_t>(b1 - b0 + 1, kPreBlk));
-    uint32_t first_dense = 0xFFFFFFFFu;
-    for (uint32_t i = C.lane; i < nb; i += 64) {
-        const uint32_t c = C.cnt[b0 + i];
-        S.cnt[i] = c;
-        if (c > kIdxCap && i < first_dense) first_dense = i;
-    }
-    const uint4 *src = reinterpret_cast<const uint4 *>(C.ent + b0 * kIdxCap);
-    uint4 *dst = reinterpret_cast<uint4 *>(S.ent);
-    for (uint32_t i = C.lane; i < nb * (kIdxCap * 2 / 16); i += 64) dst[i] = src[i];
-    S.nb = min(nb, wave_min_u32(first_dense));
+    S.nr = 0;
+    S.r0 = 0;
+    if (b > C.len) b = C.len;
+    if (a >= b) return;
+    S.r0 = run_of(C, a);
+    const uint64_t rl = run_of(C, b - 1);
+    const uint32_t nr = uint32_t(min<uint64_t>(rl - S.r0 + 1, kPreRuns));
+    for (uint32_t i = C.lane; i < nr; i += 64) S.rec[i] = C.runs[S.r0 + i];
+    S.nr = nr;
 }
 
 // First candidate in [a, b) from the preload; kNoHit if there is none,
-// kSpecMiss if the preload cannot tell.  Lanes 0-31 / 32-63 read the slots of
-// two consecutive blocks per iteration.
+// kSpecMiss if the preload cannot tell (runs outside it, a dense run first).
 __device__ uint64_t spec_first(const WalkCtx &C, const SpecIdx &S, uint64_t a, uint64_t b)
 {
-    const uint64_t bl = (b - 1) >> kIdxShift;
-    for (uint64_t blk = a >> kIdxShift; blk <= bl; blk += 2) {
-        if (blk < S.b0) return kSpecMiss;
-        const uint64_t bi = blk + (C.lane >> 5);
-        const uint64_t li = bi - S.b0;
-        const bool want = bi <= bl;
-        if (__ballot(want && li >= S.nb)) return kSpecMiss;
-        uint32_t rel = 0xFFFFFFFFu;
-        const uint32_t slot = C.lane & 31u;
-        if (want && slot < S.cnt[li]) {
-            const uint64_t pos = (bi << kIdxShift) + S.ent[li * kIdxCap + slot];
-            if (pos >= a && pos < b) rel = uint32_t(pos - a);
-        }
-        rel = wave_min_u32(rel);
-        if (rel != 0xFFFFFFFFu) return a + rel;
+    const uint64_t rl = run_of(C, b - 1);
+    for (uint64_t r = run_of(C, a); r <= rl; r += 64) {
+        const uint64_t ri = r + C.lane;
+        const bool want = ri <= rl;
+        const uint64_t li = ri - S.r0;
+        if (__ballot(want && (ri < S.r0 || li >= S.nr))) return kSpecMiss;
+        const uint64_t rec = want ? S.rec[li] : 0ull;
+        const uint64_t cand = want ? rec_first(rec, ri * C.sl, a, b) : kNoHit;
+        const uint64_t mc = __ballot(cand != kNoHit);
+        const uint64_t md = __ballot(want && cand == kNoHit && (rec & 0xFFFFu) > kRunCap);
+        const int lf = mc ? __ffsll((unsigned long long)mc) - 1 : 64;
+        const int ld = md ? __ffsll((unsigned long long)md) - 1 : 64;
+        if (ld < lf) return kSpecMiss;
+        if (lf < 64) return readlane64(cand, lf);
     }
     return kNoHit;
 }
@@ -1017,8 +967,9 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.ub = reinterpret_cast<uint64_t>(D.data);
     C.len = D.len;
     C.final_ = B.final_;
-    C.cnt = W.blk_cnt + D.blk_base;
-    C.ent = W.blk_ent + size_t(D.blk_base) * kIdxCap;
+    C.runs = W.runs + 64ull * D.task_base;
+    C.sl = B.scan_lane;
+    C.inv_sl = 1.0 / double(B.scan_lane);
     C.tab = tab;
     C.lane = threadIdx.x & 63u;
     C.laneoff = (C.lane & (kWCopies - 1u)) << 3;
@@ -1034,8 +985,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
     __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
 #if CDC_WALK_SPEC
-    __shared__ uint32_t s_pcnt[kWalkWavesPerWG][kPreBlk];
-    __shared__ __attribute__((aligned(16))) uint16_t s_pent[kWalkWavesPerWG][kPreBlk * kIdxCap];
+    __shared__ uint64_t s_prec[kWalkWavesPerWG][kPreRuns];
     __shared__ SpecBuf s_spec[kWalkWavesPerWG];
 #endif
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
@@ -1058,9 +1008,8 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
     uint64_t nx = p;
 #if CDC_WALK_SPEC
     SpecIdx S;
-    S.cnt = s_pcnt[threadIdx.x >> 6];
-    S.ent = s_pent[threadIdx.x >> 6];
-    spec_preload(C, S, (p + P.min_size) >> kIdxShift, (seg_end + P.max_size) >> kIdxShift);
+    S.rec = s_prec[threadIdx.x >> 6];
+    spec_preload(C, S, p + P.min_size, seg_end + P.max_size);
     if (C.lane == 0) dbg_ts(B, kTsW1 + 8 * g + 2);
     SpecBuf &R = s_spec[threadIdx.x >> 6];
     for (uint32_t round = 0, done = 0; !done; ++round) {
@@ -1481,8 +1430,11 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     if (seg < need) seg = need;
     seg = (seg + 15) & ~15ull;
     plan->seg = seg;
-    // Scan lane length: enough lanes to give every CU one workgroup of 8 waves
-    // (one scan workgroup fills a CU's LDS), at most 8 KiB per lane.
+    // Scan lane length: one scan workgroup per CU (a workgroup holds 112 KiB of
+    // LDS), for a grid of CUs - 8 workgroups: measured on MI355X (1 GiB, lane
+    // lengths 4-8 KiB in 128-B steps), grids of 249 and fewer run at full HBM
+    // rate while 255 workgroups ran 30 % slower per workgroup although all of
+    // them were resident from the start; lane lengths are multiples of 256 B.
     uint64_t total = 0;
     for (int i = 0; i < nbufs; ++i) total += lens[i];
     static const uint64_t cus = [] {
@@ -1492,28 +1444,31 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
             n = 256;
         return uint64_t(n);
     }();
-    uint64_t want = (total + cus * kS2Waves * 64 - 1) / (cus * kS2Waves * 64);
+    uint64_t wgs = cus > 16 ? cus - 8 : cus;
+    if (const char *env = getenv("CDC_SCAN_WGS")) {
+        const long v = atol(env);
+        if (v >= 1 && v <= 65536) wgs = uint64_t(v);
+    }
+    uint64_t want = (total + wgs * kS2Waves * 64 - 1) / (wgs * kS2Waves * 64);
     want = (want + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
     if (want < 512) want = (512 + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
     if (want > kScanLaneBytes) want = kScanLaneBytes / kLaneQuant * kLaneQuant;
     uint32_t lane = uint32_t(want);
     if (const char *env = getenv("CDC_SCAN_LANE_BYTES")) {
         const long v = atol(env);
-        if (v >= 256 && v <= (1 << 20) && v % kLaneQuant == 0) lane = uint32_t(v);
+        if (v >= 256 && v <= long(kMaxScanLane) && v % kLaneQuant == 0) lane = uint32_t(v);
     }
     plan->scan_lane = lane;
     const uint64_t task_bytes = 64ull * lane;
     plan->cap1 = uint32_t(seg / P.min_size + 3);
     plan->cap2 = 4 * plan->cap1 + 16;
-    uint64_t segs = 0, blks = 0, tasks = 0;
+    uint64_t segs = 0, tasks = 0;
     for (int i = 0; i < nbufs; ++i) {
         segs += (lens[i] + seg - 1) / seg;
-        blks += (lens[i] + kIdxBlock - 1) / kIdxBlock;
         tasks += align_tasks((lens[i] + task_bytes - 1) / task_bytes);
     }
-    if (segs >= 0xFFFF0000ull || blks >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
+    if (segs >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
     plan->total_segs = uint32_t(segs);
-    plan->total_blks = uint32_t(blks);
     plan->total_tasks = uint32_t(tasks);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -1521,8 +1476,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
         off = align_up(off + bytes, 256);
         return o;
     };
-    plan->off_blk_cnt = take(blks * 4);
-    plan->off_blk_ent = take(blks * kIdxCap * 2);
+    plan->off_runs = take(tasks * 64 * 8);
     plan->off_w1_nodes = take(segs * plan->cap1 * 8);
     plan->off_w1_cnt = take(segs * 4);
     plan->off_w2_nodes = take(segs * plan->cap2 * 8);
