@@ -228,6 +228,9 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 #ifndef CDC_SCAN_STAGE
 #define CDC_SCAN_STAGE 64
 #endif
+#ifndef CDC_SCAN_PAIRS
+#define CDC_SCAN_PAIRS 1
+#endif
 
 constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
 constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
@@ -285,11 +288,17 @@ __device__ __forceinline__ uint32_t stage_swz(uint32_t c)
 #endif
 #define DMA_PIECE(i) "global_load_lds_dwordx4 %" #i ", %[base]" DMA_AUX "\n\t" DMA_PAD
 #define DMA_NEXT "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-__device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uint32_t (&off)[kL])
+__device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, const uint32_t (&off)[kL])
 {
+    // wave-uniform operands pinned to SGPRs (under VGPR pressure the compiler
+    // may otherwise keep them in VGPRs, which the "s" constraint does not stop);
+    // the statement opens with s_nop 4 (VALU-written SGPR read as a VMEM base)
+    const uint64_t base = (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(base_in >> 32)))) << 32) |
+                          uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(base_in)));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(dst_in);
     uint32_t keep;
     if constexpr (kL == 8) {
-        asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+        asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
                      DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4) DMA_NEXT
                      DMA_PIECE(5) DMA_NEXT DMA_PIECE(6) DMA_NEXT DMA_PIECE(7) DMA_NEXT DMA_PIECE(8)
                      "s_mov_b32 m0, %[keep]\n\ts_nop 1"
@@ -298,14 +307,14 @@ __device__ __forceinline__ void dma_stage(uint64_t base, uint32_t dst, const uin
                        "v"(off[7]), [base] "s"(base), [dst] "s"(dst)
                      : "memory", "scc");
     } else if constexpr (kL == 4) {
-        asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+        asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
                      DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4)
                      "s_mov_b32 m0, %[keep]\n\ts_nop 1"
                      : [keep] "=&s"(keep)
                      : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), [base] "s"(base), [dst] "s"(dst)
                      : "memory", "scc");
     } else {
-        asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+        asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
                      DMA_PIECE(1) DMA_NEXT DMA_PIECE(2)
                      "s_mov_b32 m0, %[keep]\n\ts_nop 1"
                      : [keep] "=&s"(keep)
@@ -379,20 +388,81 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     const int64_t s = int64_t((seg0 + lane) * sl);
     const int64_t e = s < int64_t(D.len) ? min(s + int64_t(sl), int64_t(D.len)) : s;
     // stage t of lane c covers [A(c) - 64 + kStage t, + kStage), A(c) = align16(ub + (seg0 + c) sl)
-    const uint32_t T = uint32_t((sl + 64u + (ub & 15u) + kStage - 1u) / kStage);
-    const uint64_t wb = ((ub + seg0 * sl) & ~15ull) - 64u;   // lane 0's first stage
+    // Staging starts kLead bytes before the run (>= W - 1 warm-up bytes); with
+    // pair staging 128, so that its 128-B DMA chunks are whole HBM lines on a
+    // 128-B aligned buffer (64-B aligned chunks straddle two lines: 40 % slower).
+    constexpr uint32_t kLead = CDC_SCAN_PAIRS ? 128u : 64u;
+    const uint32_t T = uint32_t((sl + kLead + (ub & 15u) + kStage - 1u) / kStage);
+    const uint64_t wb = ((ub + seg0 * sl) & ~15ull) - kLead;  // lane 0's first stage
     const uint64_t base = wb > lo_ok ? wb : lo_ok;           // wave-uniform DMA base
     const uint64_t limw = hi_ok - 16u - base;                // last in-bounds piece (lane 0 is in bounds)
     const uint32_t lim = limw > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(limw);
+    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kNBuf * kStageBytes;
+#if CDC_SCAN_PAIRS
+    // Pair staging: DMA t carries 128 B (whole lines) of each of the 32 runs
+    // of half t & 1 of the wave (4 instructions of 8 runs x 128 B), which reads
+    // HBM ~14 % faster than 16 runs x 64 B (tools/ubench_mem.hip).  Half 1 runs
+    // one stage behind half 0; a lane reloads every other stage, keeping the
+    // second 64 B in registers.  Slot layout: run row r = lane & 31 at 128 r,
+    // piece p at 16 (p ^ ((r >> 1) & 7)) (conflict-free ds_read_b128).
+    static_assert(kStage == 64 && kL == 4, "pair staging: 64-B stages");
+    const uint32_t half = lane >> 5;
+    const uint32_t row = lane & 31u, swz = (row >> 1) & 7u;
+    // per-lane piece offsets of the two halves' DMAs (separate arrays, selected
+    // by bit masks: a runtime-indexed [2][4] array went to LDS)
+    uint32_t off0[4], off1[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t r = 8u * j + lane / 8u;
+        const uint32_t k = (lane % 8u) ^ ((r >> 1) & 7u);
+        off0[j] = uint32_t((((ub + (seg0 + r) * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
+        off1[j] = uint32_t((((ub + (seg0 + 32u + r) * sl) & ~15ull) - kLead + 16u * k) - base);
+#if CDC_DIAG_OLD_ADDR  // diagnostic: the 16 runs x 64 B mapping (wrong data, same timing structure)
+        {
+            const uint64_t q2 = seg0 + 16u * j + lane / 4u;
+            off0[j] = off1[j] = uint32_t((((ub + q2 * sl) & ~15ull) - kLead + 16u * (lane % 4u)) - base);
+        }
+#endif
+    }
+    auto issue = [&](uint32_t t) {
+#if CDC_DIAG_NO_DMA
+        if (t >= 2 * kNBuf) return;
+#endif
+#if CDC_DIAG_OLD_ADDR
+        const uint32_t hh = 0, adv = kStage * t, m = 0;
+#else
+        const uint32_t hh = t & 1u, adv = kStage * (t - hh), m = 0u - hh;
+#endif
+        uint32_t eff[kL];
+#pragma unroll
+        for (uint32_t j = 0; j < kL; ++j) eff[j] = min(((off1[j] & m) | (off0[j] & ~m)) + adv, lim);
+        dma_stage(base, ring + (t % kNBuf) * kStageBytes, eff);
+    };
+    uint4 hold[4] = {};
+    // data of stage t for this lane: a fresh 128 B from the slot every other stage
+    auto load_stage = [&](uint32_t t, uint4 (&dd)[kGroups]) {
+        if ((t & 1u) == half) {
+            const char *buf = s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + row * 128u;
+#pragma unroll
+            for (uint32_t g = 0; g < 4; ++g) dd[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+#pragma unroll
+            for (uint32_t g = 0; g < 4; ++g) hold[g] = *reinterpret_cast<const uint4 *>(buf + 16u * ((g + 4) ^ swz));
+        } else {
+#pragma unroll
+            for (uint32_t g = 0; g < 4; ++g) dd[g] = hold[g];
+        }
+    };
+    const uint32_t TT = T + 1;  // half 1 runs one stage behind
+    const int32_t lag = int32_t(kStage * half);
+#else
     // the kL pieces this lane loads: DMA j carries piece (lane % kL) ^ swz of run q = seg0 + (64/kL) j + lane/kL
     uint32_t off[kL];
 #pragma unroll
     for (uint32_t j = 0; j < kL; ++j) {
         const uint64_t q = seg0 + (64u / kL) * j + lane / kL;
         const uint32_t k = (lane % kL) ^ stage_swz(uint32_t(q - seg0));
-        off[j] = uint32_t((((ub + q * sl) & ~15ull) - 64u + 16u * k) - base);  // wraps below base: clamped
+        off[j] = uint32_t((((ub + q * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
     }
-    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kNBuf * kStageBytes;
     auto issue = [&](uint32_t t) {
 #if CDC_DIAG_NO_DMA
         if (t >= kNBuf) return;  // diagnostic: compute over the first ring fill again and again
@@ -402,44 +472,49 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
         for (uint32_t j = 0; j < kL; ++j) eff[j] = min(off[j] + kStage * t, lim);
         dma_stage(base, ring + (t % kNBuf) * kStageBytes, eff);
     };
-    auto slot_of = [&](uint32_t t) -> const char * {
-        return s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + lane * kStage;
+    const uint32_t swz = stage_swz(lane);
+    auto load_stage = [&](uint32_t t, uint4 (&dd)[kGroups]) {
+        const char *buf = s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + lane * kStage;
+#pragma unroll
+        for (uint32_t g = 0; g < kGroups; ++g) dd[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
     };
+    const uint32_t TT = T;
+    const int32_t lag = 0;
+#endif
     const uint32_t vhi = to_vgpr(P.fs_hi);
     const uint32_t xlo = P.fs_lo, xhi = P.fs_hi;
-    const uint32_t swz = stage_swz(lane);
     // buffer-relative position of this lane's first staged byte
-    const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - 64u) - int64_t(ub);
+    const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
 
     // Every stage's data is copied into registers (d / dn) before its slot is
     // needed again, so slot t % kNBuf is refilled with stage t + kNBuf as soon
     // as stage t's reads have retired (after group 0 of stage t): kNBuf stages
     // in flight per wave with a kNBuf-slot ring.
-    for (uint32_t t = 0; t < kNBuf && t < T; ++t) issue(t);
-    if (T > kAhead) wait_vmcnt<kL * kAhead>();
+    for (uint32_t t = 0; t < kNBuf && t < TT; ++t) issue(t);
+    if (TT > kAhead) wait_vmcnt<kL * kAhead>();
     else wait_vmcnt<0>();
     uint4 d[kGroups];
-    {
-        const char *buf = slot_of(0);
-#pragma unroll
-        for (uint32_t g = 0; g < kGroups; ++g) d[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
-        asm volatile("" ::: "memory");  // the slot reads issue before any gather (see the lgkmcnt below)
-    }
+    load_stage(0, d);
+    asm volatile("" ::: "memory");  // the slot reads issue before any gather (see the lgkmcnt below)
     // gathers double-buffered by group parity: group gi rolls gv[gi & 1] while
     // the next group's values land in gv[(gi + 1) & 1]; a recheck reads the
     // rolled group's values from registers.
+#if CDC_GV_SINGLE
+    uint64_t gv[1][16];  // single-buffered: a recheck re-gathers (fewer VGPRs, 4 waves per SIMD)
+#else
     uint64_t gv[2][16];
+#endif
 #pragma unroll
     for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
     uint64_t fp = 0;
     uint64_t rec = 0;  // this lane's run record
     const int32_t len = int32_t(e - s);
-    const int32_t rr0 = int32_t(rel0 - s);  // run-relative position of the lane's first staged byte
-    for (uint32_t t = 0; t < T; ++t) {
+    const int32_t rr0 = int32_t(rel0 - s) - lag;  // run-relative position of the lane's stage-0 bytes
+    for (uint32_t t = 0; t < TT; ++t) {
         uint4 dn[kGroups];
 #pragma unroll
         for (uint32_t gi = 0; gi < kGroups; ++gi) {
-            if (gi == 1 && t + kNBuf < T) {
+            if (gi == 1 && t + kNBuf < TT) {
                 // >= 16 gathers were issued after stage t's slot reads: lgkmcnt(15)
                 // retires those reads, and the slot can take stage t + kNBuf.
                 asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
@@ -447,16 +522,19 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
             }
             if (gi + 1 == kGroups) {
                 // next stage's data: landed once at most kNBuf - 1 younger stages are in flight
-                if (t + kNBuf < T) wait_vmcnt<kL * kAhead>();
+                if (t + kNBuf < TT) wait_vmcnt<kL * kAhead>();
                 else wait_vmcnt<0>();
-                const char *buf = slot_of(t + 1);
-#pragma unroll
-                for (uint32_t g = 0; g < kGroups; ++g) dn[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
+                load_stage(t + 1, dn);
                 asm volatile("" ::: "memory");
             }
             const uint4 &nx = gi + 1 < kGroups ? d[gi + 1] : dn[0];
+#if CDC_GV_SINGLE
+            uint64_t (&cur)[16] = gv[0];
+            uint64_t (&nxt)[16] = gv[0];
+#else
             uint64_t (&cur)[16] = gv[gi & 1];
             uint64_t (&nxt)[16] = gv[(gi + 1) & 1];
+#endif
 #if CDC_DIAG_NO_COMPUTE
             fp += nx.x ^ d[gi].w;  // diagnostic: staging only
             if (fp == 0x123456789ull) rec = fp;
@@ -483,7 +561,16 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
 #else
             if (acc == 0) [[unlikely]]
 #endif
+            {
+#if CDC_GV_SINGLE
+                uint64_t g2[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) g2[k] = lds_gear(tab, gear_addr(laneoff, word_of(d[gi], k >> 2), k));
+                recheck_group(f0, g2, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
+#else
                 recheck_group(f0, cur, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
+#endif
+            }
         }
 #pragma unroll
         for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
