@@ -7,7 +7,7 @@ import sys
 d = sys.argv[1]
 ksub = sys.argv[2] if len(sys.argv) > 2 else "k_scan"
 agg = collections.defaultdict(list)
-for p in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+for p in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv") + glob.glob(f"{d}/run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
         if ksub in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
