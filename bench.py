@@ -122,6 +122,62 @@ def load_traffic(workload):
         return None
 
 
+def digest_leg(torch, batch, bufs, reps, check):
+    """Per-chunk SHA-256 + byte histogram (processChunk, snapshot/backup.go:594-629)
+    over the device cut lists of the pass: device-resident, events around the
+    digest kernels.  Not part of `value`.  On rank 0 of a 1-GPU run the first
+    buffer's digests are checked against hashlib on a bounded sample, and hashlib
+    (1 core) is timed on the same sample as its CPU baseline."""
+    import hashlib
+    import numpy as np
+    from plakar_amd import hashing
+    cut_lists = [batch.cuts[i] for i in range(batch.n)]
+    res_rows = [batch.res[i] for i in range(batch.n)]
+
+    def run():  # every buffer's chunks in one launch group
+        return hashing.chunk_digests_batch(bufs, cut_lists, res_rows)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        out = run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    total = sum(t.numel() for t in bufs)
+    cuts, _ = batch.results()
+    longest = max(int(c[:, 1].max().item()) for c in cuts if c.shape[0])
+    nchunks = sum(int(c.shape[0]) for c in cuts)
+    d = dict(value=round(total / (ms * 1e-3) / GIB, 2), unit="GiB/s", ms_per_pass=round(ms, 3), chunks=nchunks,
+             longest_chunk=longest, kernel="k_chunk_digest (SHA-256 + 256-bin histogram, one lane per chunk)",
+             bound="one lane's serial chain: the longest chunk's 64-B blocks x ~1,480 VALU at one wave per SIMD")
+    if check:
+        host = bufs[0][:min(bufs[0].numel(), 256 << 20)].cpu().numpy()
+        c0 = cuts[0].cpu().numpy()
+        dg = out[0][0][:c0.shape[0]].cpu().numpy()
+        hs = out[0][1][:c0.shape[0]].cpu().numpy()
+        ok, nbytes, t0 = True, 0, time.perf_counter()
+        for i, (o, n) in enumerate(c0):
+            if o + n > host.size:
+                break
+            part = host[o:o + n]
+            ok &= hashlib.sha256(part.tobytes()).digest() == bytes(dg[i])
+            ok &= bool((np.bincount(part, minlength=256) == hs[i]).all())
+            nbytes += int(n)
+        el = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for i, (o, n) in enumerate(c0):
+            if o + n > host.size:
+                break
+            hashlib.sha256(host[o:o + n].tobytes()).digest()
+        el = time.perf_counter() - t0
+        d["parity_vs_hashlib"] = ok
+        d["cpu_baseline"] = dict(value=round(nbytes / el / GIB, 3), unit="GiB/s", cores=1, kind="hashlib",
+                                 sample=f"SHA-256 of the first {nbytes >> 20} MiB of chunks of buffer 0, 1 thread")
+    return d
+
+
 def cpu_baseline(bufs_host, cuts_dev, opts, seconds):
     """The CPU oracle (scalar C restatement of the reference chunker, 1 thread)
     timed on a bounded sample of the same workload; also checks that the GPU
@@ -166,6 +222,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="device workloads: consecutive steps alternate over this many streams, each with its "
                          "own workspace, so one batch's resolution kernels overlap the next batch's scan")
+    ap.add_argument("--digest-reps", type=int, default=3,
+                    help="reps of the per-chunk SHA-256 + histogram leg (SURVEY.md 8f; 0 = skip)")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="reps of the PCIe-inclusive host-buffer leg (0 = skip)")
     args = ap.parse_args()
@@ -278,6 +336,10 @@ def main():
                     timed_passes=n,
                     pipeline_avg_ms=round(pipe_avg_ms, 4))
 
+    digest = None
+    if not host_mode and args.digest_reps > 0:
+        digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0 and world == 1)
+
     baseline, parity, e2e = None, None, None
     if rank == 0 and world == 1:
         import numpy as np
@@ -332,6 +394,7 @@ def main():
             "cpu_baseline": baseline,
             "parity_vs_oracle": parity,
             "e2e_host_path": e2e,
+            "chunk_digests": digest,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -149,6 +149,29 @@ int cdc_chunk_device_batch_async(int device, const void *const *d_data, const ui
                                  cdc_result *const *d_results, void *d_workspace,
                                  uint64_t workspace_bytes, void *stream);
 
+/* ---- per-chunk digests: the per-chunk work of snapshot/backup.go processChunk --
+ * For each chunk of a device cut list (offsets relative to d_data), the
+ * SHA-256 of the chunk's bytes into d_digests (32 bytes per chunk: the
+ * chunkHasher.Sum of snapshot/backup.go:604-606, hashing "SHA256" =
+ * crypto/sha256, hashing/hashing.go:31-36) and, when d_hist is not NULL, the
+ * chunk's byte histogram into d_hist (256 uint32 per chunk: the freq[] that
+ * entropy() counts, snapshot/backup.go:548-557; the float64 entropy and the
+ * normalised Distribution are the caller's, since math.Log2 defines them).
+ * The chunk count is min(cut_cap, d_result->ncuts) when d_result is not NULL
+ * (a cut list still on the device), else cut_cap.  An empty chunk hashes to
+ * SHA-256(""), like processChunk([]byte{}) for an empty file (backup.go:631).
+ * Asynchronous on `stream`; d_digests / d_hist hold cut_cap entries. */
+int cdc_chunk_digests_device_async(int device, const void *d_data, uint64_t len, const cdc_cut *d_cuts,
+                                   uint64_t cut_cap, const cdc_result *d_result, uint8_t *d_digests,
+                                   uint32_t *d_hist, void *stream);
+/* Batched form: every chunk of nbufs buffers hashes in one launch group (the
+ * time of a launch is that of its longest chunk, so batch).  d_results and
+ * d_hist may be NULL; d_hist entries are all NULL or all set. */
+int cdc_chunk_digests_device_batch_async(int device, const void *const *d_data, const uint64_t *lens, int nbufs,
+                                         const cdc_cut *const *d_cuts, const uint64_t *cut_caps,
+                                         const cdc_result *const *d_results, uint8_t *const *d_digests,
+                                         uint32_t *const *d_hist, void *stream);
+
 /* ---- streaming chunker: chunkers.NewChunker / (*Chunker).Next -----------------
  * Push model, so cgo never hands a Go pointer to asynchronous HIP work: the
  * caller appends stream bytes into a pinned staging window the library owns

@@ -92,6 +92,14 @@ SIGNATURES = {
                                        _P(ctypes.c_void_p)]),
     "cdc_chunker_next": (ctypes.c_int, [ctypes.c_void_p, _P(_u8p), _P(ctypes.c_uint64)]),
     "cdc_chunker_free": (None, [ctypes.c_void_p]),
+    "cdc_chunk_digests_device_async": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                                      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "cdc_chunk_digests_device_batch_async": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_void_p),
+                                                            _P(ctypes.c_uint64), ctypes.c_int,
+                                                            _P(ctypes.c_void_p), _P(ctypes.c_uint64),
+                                                            _P(ctypes.c_void_p), _P(ctypes.c_void_p),
+                                                            _P(ctypes.c_void_p), ctypes.c_void_p]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),

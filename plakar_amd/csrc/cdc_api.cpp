@@ -678,6 +678,43 @@ int cdc_chunk_device_batch_async(int device, const void *const *d_data, const ui
     return CDC_OK;
 }
 
+int cdc_chunk_digests_device_batch_async(int device, const void *const *d_data, const uint64_t *lens, int nbufs,
+                                         const cdc_cut *const *d_cuts, const uint64_t *cut_caps,
+                                         const cdc_result *const *d_results, uint8_t *const *d_digests,
+                                         uint32_t *const *d_hist, void *stream)
+{
+    if (nbufs < 0 || (nbufs > 0 && (!d_data || !lens || !d_cuts || !cut_caps || !d_digests))) return CDC_E_INVALID;
+    for (int i = 0; i < nbufs; ++i) {
+        if ((lens[i] && !d_data[i]) || (cut_caps[i] && (!d_cuts[i] || !d_digests[i]))) return CDC_E_INVALID;
+        if (d_hist && (d_hist[i] == nullptr) != (d_hist[0] == nullptr)) return CDC_E_INVALID;
+    }
+    DeviceCtx *ctx = nullptr;
+    int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    for (int i0 = 0; i0 < nbufs; i0 += kMaxBufsPerLaunch) {
+        DigestBatch DB;
+        std::memset(&DB, 0, sizeof(DB));
+        DB.nbufs = uint32_t(std::min(kMaxBufsPerLaunch, nbufs - i0));
+        for (uint32_t j = 0; j < DB.nbufs; ++j) {
+            const int i = i0 + int(j);
+            DB.b[j] = DigestBuf{static_cast<const uint8_t *>(d_data[i]), lens[i], d_cuts[i], cut_caps[i],
+                                d_results ? d_results[i] : nullptr, d_digests[i], d_hist ? d_hist[i] : nullptr};
+        }
+        st = launch_digests(DB, stream);
+        if (st != CDC_OK) return st;
+    }
+    return CDC_OK;
+}
+
+int cdc_chunk_digests_device_async(int device, const void *d_data, uint64_t len, const cdc_cut *d_cuts,
+                                   uint64_t cut_cap, const cdc_result *d_result, uint8_t *d_digests,
+                                   uint32_t *d_hist, void *stream)
+{
+    return cdc_chunk_digests_device_batch_async(device, &d_data, &len, 1, &d_cuts, &cut_cap, &d_result, &d_digests,
+                                                d_hist ? &d_hist : nullptr, stream);
+}
+
 int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out, uint64_t out_cap,
               uint64_t *out_counts, uint64_t *out_needed)
 {

@@ -102,5 +102,20 @@ struct Plan {
 uint64_t align_tasks(uint64_t tasks);
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan);
 int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream);
+// cdc_digest.hip: per-chunk SHA-256 (+ optional byte histogram) of device cut lists.
+struct DigestBuf {
+    const uint8_t *data;
+    uint64_t len;
+    const cdc_cut *cuts;
+    uint64_t cap;
+    const cdc_result *res;  // nullable: count = min(cap, res->ncuts)
+    uint8_t *digests;       // 32 B per chunk
+    uint32_t *hist;         // 256 u32 per chunk, or null (all or none in one launch)
+};
+struct DigestBatch {
+    uint32_t nbufs;
+    DigestBuf b[kMaxBufsPerLaunch];
+};
+int launch_digests(const DigestBatch &DB, void *stream);
 
 }  // namespace cdc

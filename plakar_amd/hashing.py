@@ -1,0 +1,144 @@
+"""Mirror of plakar's hashing package and of the per-chunk work of
+snapshot/backup.go processChunk, on the device.
+
+    hashing/hashing.go:9-29      Configuration, DefaultConfiguration,
+                                 LookupDefaultConfiguration
+    snapshot/backup.go:548-569   entropy(data) -> (entropy, freq[256])
+    snapshot/backup.go:594-629   processChunk: chunk SHA-256, entropy, the
+                                 normalised byte distribution -> objects.Chunk
+
+chunk_digests() runs the HIP kernel of libplakar_cdc.so
+(cdc_chunk_digests_device_async): one SHA-256 and one 256-bin histogram per
+chunk of a device cut list.  The float64 entropy is computed here, on the host,
+with the reference's formula and summation order, from the exact integer
+histogram.
+"""
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import List
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+@dataclass
+class Configuration:
+    """hashing.Configuration (hashing/hashing.go:9-12)."""
+    Algorithm: str
+    Bits: int
+
+
+def LookupDefaultConfiguration(algorithm):
+    """hashing.LookupDefaultConfiguration (hashing/hashing.go:19-29)."""
+    if algorithm == "SHA256":
+        return Configuration("SHA256", 256), None
+    return None, ValueError(f"unknown hashing algorithm: {algorithm}")
+
+
+def DefaultConfiguration():
+    """hashing.DefaultConfiguration (hashing/hashing.go:14-17)."""
+    return LookupDefaultConfiguration("SHA256")[0]
+
+
+def chunk_digests(data, cuts, result=None, hist=True, stream=None):
+    """SHA-256 (and byte histogram) of every chunk of a device buffer.
+
+    data: contiguous uint8 CUDA tensor; cuts: (n, 2) int64 CUDA tensor of
+    (offset, length) as the device path returns them (or its raw cdc_cut
+    storage); result: optional int64 CUDA tensor row (ncuts, consumed,
+    status, needed) bounding the count on the device.  Returns (digests
+    uint8 (n, 32), histograms int32 (n, 256) or None) on the device;
+    asynchronous on `stream` like the rest of the device path.
+    """
+    if data.dtype != torch.uint8 or not data.is_cuda or not data.is_contiguous():
+        raise ValueError("expected a contiguous uint8 CUDA tensor")
+    if cuts.dtype != torch.int64 or cuts.dim() != 2 or cuts.shape[1] != 2 or not cuts.is_contiguous():
+        raise ValueError("expected an (n, 2) contiguous int64 cut tensor")
+    n = cuts.shape[0]
+    dev = data.device
+    digests = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    h = torch.empty((n, 256), dtype=torch.int32, device=dev) if hist else None
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    check(lib().cdc_chunk_digests_device_async(
+        dev.index, ctypes.c_void_p(data.data_ptr()), data.numel(), ctypes.c_void_p(cuts.data_ptr()), n,
+        ctypes.c_void_p(result.data_ptr() if result is not None else 0), ctypes.c_void_p(digests.data_ptr()),
+        ctypes.c_void_p(h.data_ptr() if h is not None else 0), ctypes.c_void_p(stream.cuda_stream)), "digests")
+    return digests, h
+
+
+def chunk_digests_batch(datas, cut_lists, results=None, hist=True, stream=None):
+    """chunk_digests() for several buffers in one launch group (every chunk of
+    every buffer hashes in parallel: a launch lasts as long as its longest
+    chunk, so batching is what gives throughput).  Returns a list of
+    (digests, histograms) per buffer."""
+    n = len(datas)
+    if n == 0:
+        return []
+    dev = datas[0].device
+    for t, c in zip(datas, cut_lists):
+        if t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("expected contiguous uint8 CUDA tensors")
+        if c.dtype != torch.int64 or c.dim() != 2 or c.shape[1] != 2 or not c.is_contiguous():
+            raise ValueError("expected (n, 2) contiguous int64 cut tensors")
+    outs = [(torch.empty((c.shape[0], 32), dtype=torch.uint8, device=dev),
+             torch.empty((c.shape[0], 256), dtype=torch.int32, device=dev) if hist else None) for c in cut_lists]
+    V = ctypes.c_void_p
+    arr = lambda xs: (V * n)(*xs)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    check(lib().cdc_chunk_digests_device_batch_async(
+        dev.index, arr([t.data_ptr() for t in datas]), (ctypes.c_uint64 * n)(*[t.numel() for t in datas]), n,
+        arr([c.data_ptr() for c in cut_lists]), (ctypes.c_uint64 * n)(*[c.shape[0] for c in cut_lists]),
+        arr([r.data_ptr() for r in results]) if results is not None else None,
+        arr([o[0].data_ptr() for o in outs]), arr([o[1].data_ptr() for o in outs]) if hist else None,
+        V(stream.cuda_stream)), "digests")
+    return outs
+
+
+def entropy_from_freq(freq, size):
+    """entropy() of snapshot/backup.go:548-569 from its frequency table: the
+    same float64 terms in the same order (bins 0..255)."""
+    if size == 0:
+        return 0.0
+    e = 0.0
+    data_size = float(size)
+    for f in freq:
+        if f > 0:
+            p = float(f) / data_size
+            e -= p * math.log2(p)
+    return e
+
+
+@dataclass
+class Chunk:
+    """objects.Chunk (objects/objects.go:73-79)."""
+    Checksum: bytes
+    Length: int
+    Entropy: float
+    Distribution: List[float] = field(default_factory=list)
+
+
+def chunk_records(data, cuts, result=None):
+    """processChunk's per-chunk records (snapshot/backup.go:594-629) for every
+    chunk of a device cut list: Checksum and the histogram on the device,
+    Entropy and Distribution (freq / len) on the host."""
+    digests, hist = chunk_digests(data, cuts, result)
+    torch.cuda.synchronize(data.device)
+    lens = cuts[:, 1].cpu().tolist()
+    dg = digests.cpu().numpy()
+    hs = hist.cpu().numpy()
+    out = []
+    for i, n in enumerate(lens):
+        freq = hs[i].tolist()
+        dist = [float(f) / n for f in freq] if n > 0 else [0.0] * 256
+        out.append(Chunk(bytes(dg[i]), int(n), entropy_from_freq(freq, n), dist))
+    return out
+
+
+__all__ = ["Configuration", "LookupDefaultConfiguration", "DefaultConfiguration", "chunk_digests",
+           "chunk_digests_batch",
+           "entropy_from_freq", "Chunk", "chunk_records", "_lib"]
