@@ -7,16 +7,14 @@
 // left to the caller, whose math.Log2 and summation order define it.
 //
 // SHA-256 is a serial chain over a message's 64-byte blocks, so the unit of
-// parallelism is the chunk: one lane per chunk (FIPS 180-4, multi-buffer
-// style), one wave per workgroup.  Each lane reads its chunk as aligned
-// dwords and builds the big-endian message words with one v_perm_b32 per
-// word (funnel shift + byte swap).  The histogram is kept per lane in LDS,
-// transposed (bin b of lane l at 4 * (64 b + l)) so that every lane always
-// hits its own bank: 64 KiB per wave.
+// parallelism is the chunk: one chunk per lane (FIPS 180-4, multi-buffer
+// style), and each chunk is worked on by two lanes of two waves, a producer
+// (loads, padding, histogram, message schedule) and a consumer (the rounds),
+// see k_chunk_digest below.
 //
-// Roofline: VALU-bound (~1,400 VALU per 64-byte block per lane); the time is
-// set by the longest chunk of the launch (blocks x dependent-chain latency),
-// see DESIGN.md.
+// Bound: the consumer's chain, ~905 VALU per 64-byte block (14 per round,
+// which is what three-input adds, bitop3 and alignbit allow), at one wave per
+// SIMD; a launch lasts as long as its longest chunk.
 #include <hip/hip_runtime.h>
 
 #include "cdc_internal.h"
@@ -39,164 +37,216 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU
 }
 
-// One SHA-256 compression of the 16 big-endian words w into h.
-__device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16])
+// Two waves per workgroup of 64 chunks, one lane per chunk in each:
+//   wave 1, the producer: loads block b + 1's words while it works on block b,
+//     builds the big-endian words (v_perm funnel shift + byte swap), pads the
+//     final block(s), counts the histogram, and expands the message schedule
+//     W[0..63] into an LDS ring stage;
+//   wave 0, the consumer: the 64 rounds of block b - 1 from the other stage.
+// One s_barrier per block.  The consumer's chain is ~14 VALU per round
+// instead of ~25 when one lane did everything; the producer's ~700 VALU fit
+// under it on another SIMD.
+constexpr uint32_t kShaRing = 2;                                   // stages
+constexpr uint32_t kRingBytes = kShaRing * 64u * 64u * 4u;         // 32 KiB: [stage][word quad][lane] uint4
+// The histogram: u16 halves, lanes l and l + 32 share the dword of bin b at
+// 4 * (32 b + (l & 31)) (every access of a wave stays in its own bank pair),
+// 32 KiB; flushed to the u32 output every kFlushBlocks blocks so that a half
+// never passes 64 x 1023 < 65536 counts.
+constexpr uint32_t kHistPairBytes = 256u * 32u * 4u;
+constexpr uint64_t kFlushBlocks = 1023;
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
-    for (int t = 0; t < 64; ++t) {
-        uint32_t wt;
-        if (t < 16) {
-            wt = w[t];
-        } else {
-            const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-            wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
-            w[t & 15] = wt;
-        }
-        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-        const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);   // (e & f) | (~e & g)
-        const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
-        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);   // majority
-        hh = g;
-        g = f;
-        f = e;
-        e = d + t1;
-        d = c;
-        c = b;
-        b = a;
-        a = t1 + S0 + mj;
-    }
-    h[0] += a;
-    h[1] += b;
-    h[2] += c;
-    h[3] += d;
-    h[4] += e;
-    h[5] += f;
-    h[6] += g;
-    h[7] += hh;
+    for (int o = 32; o; o >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), o)));
+    return v;
 }
 
-constexpr uint32_t kDigestHistBytes = 256u * 64u * 4u;  // 64 KiB: one wave's transposed histograms
-
-// grid (ceil(max cap / 64), nbufs) workgroups of 64: lane i of workgroup
-// (w, b) owns chunk 64 w + i of buffer b, so every chunk of the launch group
-// hashes in parallel (a launch lasts as long as its longest chunk).
 template <bool HIST>
-__global__ __launch_bounds__(64) void k_chunk_digest(const DigestBatch DB)
+__global__ __launch_bounds__(128) void k_chunk_digest(const DigestBatch DB)
 {
-    extern __shared__ uint32_t s_hist[];  // [256][64] when HIST
+    extern __shared__ uint4 s_mem[];
+    uint4 *ring = s_mem;                                                   // [kShaRing][16][64]
+    uint32_t *s_hist = reinterpret_cast<uint32_t *>(s_mem + kShaRing * 16 * 64);  // [256][32]
     const DigestBuf &B = DB.b[blockIdx.y];
-    const uint8_t *data = B.data;
-    const uint64_t len = B.len, cap = B.cap;
-    const cdc_cut *cuts = B.cuts;
-    const cdc_result *res = B.res;
-    uint8_t *digests = B.digests;
-    uint32_t *hist = B.hist;
-    const uint32_t lane = threadIdx.x;
-    uint64_t n_cuts = cap;
-    if (res) n_cuts = min<uint64_t>(cap, uint64_t(res->ncuts));
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
+    uint64_t n_cuts = B.cap;
+    if (B.res) n_cuts = min<uint64_t>(B.cap, uint64_t(B.res->ncuts));
+    if (uint64_t(blockIdx.x) * 64u >= n_cuts) return;  // whole workgroup: no barrier is left waiting
     const uint64_t i = uint64_t(blockIdx.x) * 64u + lane;
-    if (HIST) {
-#pragma unroll 8
-        for (uint32_t b = 0; b < 256; ++b) s_hist[b * 64u + lane] = 0;
+    const bool valid = i < n_cuts;
+    uint64_t n = 0, off = 0;
+    if (valid) {
+        const cdc_cut cut = B.cuts[i];
+        off = cut.offset;
+        n = cut.length;
+        if (off > B.len) n = 0;
+        else if (n > B.len - off) n = B.len - off;  // clipped to the buffer (a malformed list must not fault)
     }
-    if (i >= n_cuts) return;
-    if (HIST && !hist) return;  // launch-wide HIST, this buffer wants digests only: not a case the API makes
-    const cdc_cut cut = cuts[i];
-    uint64_t n = cut.length;
-    if (cut.offset > len) n = 0;
-    else if (n > len - cut.offset) n = len - cut.offset;  // clipped to the buffer (a malformed list must not fault)
-    const uint8_t *p = data + cut.offset;
-    auto count = [&](uint32_t word_be, uint32_t nbytes) {  // histogram of the first nbytes of a big-endian word
-        if (!HIST) return;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            if (j < nbytes) {
-                const uint32_t bv = (word_be >> (24u - 8u * j)) & 0xFFu;
-                __hip_atomic_fetch_add(&s_hist[bv * 64u + lane], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-    };
+    // blocks of the padded message: the full ones, then 1 or 2
+    const uint64_t nb = valid ? n / 64u + ((n % 64u) <= 55u ? 1u : 2u) : 0u;
+    const uint64_t NB = wave_max(uint32_t(min<uint64_t>(nb, 0xFFFFFFFFull)));  // both waves: same lanes, same bound
 
-    uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                     0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    uint32_t w[16];
-    // full blocks: aligned dword loads, v_perm funnel shift + byte swap
-    const uint64_t nfull = n / 64u;
-    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
-    const uint32_t sel = (sh << 24) | ((sh + 1u) << 16) | ((sh + 2u) << 8) | (sh + 3u);
-    // derived from the kernel argument (not through an integer), so the loads
-    // are global_load, not flat
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(p - sh);
-    if (nfull) {
-        // software pipeline: block b + 1's words are loaded before block b is
-        // compressed (~1,400 VALU), so the load latency is not exposed
-        // Block b uses dwords q[16 b .. 16 b + 16].  With sh == 0 the last one
-        // holds no byte of the block (v_perm selects only `lo`), and for the
-        // last block it can lie past the buffer end: it is not loaded then.
-        auto load16 = [&](const uint32_t *qb, bool last, uint32_t (&x)[16]) {
-#pragma unroll
-            for (int k = 0; k < 15; ++k) x[k] = qb[k];
-            x[15] = qb[(last && sh == 0) ? 14 : 15];  // index select: no load past the chunk
+    if (producer) {
+        const uint8_t *p = B.data + (valid ? off : 0);
+        const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+        const uint32_t sel = (sh << 24) | ((sh + 1u) << 16) | ((sh + 2u) << 8) | (sh + 3u);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(p - sh);
+        const uint64_t lastq = n ? (sh + n - 1u) >> 2 : 0;  // last dword holding a byte of the chunk
+        const uint32_t hoff = (lane & 31u) * 4u, hinc = 1u << (16u * (lane >> 5));
+        if (HIST) {
+#pragma unroll 8
+            for (uint32_t b = 0; b < 256; b += 2) s_hist[b * 32u + lane] = 0;  // 64 lanes, two bins a step
+        }
+        auto count1 = [&](uint32_t byte) {
+            __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s_hist) + ((byte << 7) | hoff)),
+                                   hinc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         };
-        uint32_t lo = q[0];
-        const uint32_t *qb = q + 1;
-        uint32_t nx[16];
-        load16(qb, nfull == 1, nx);
-        for (uint64_t blk = 0; blk < nfull; ++blk) {
-            uint32_t dw[16];
+        bool flushed = false;
+        auto flush = [&]() {
+            if (valid && B.hist) {
+                uint4 *ho = reinterpret_cast<uint4 *>(B.hist + i * 256u);
+                const uint32_t hs = 16u * (lane >> 5);
+#pragma unroll 4
+                for (uint32_t b = 0; b < 256; b += 4) {
+                    uint4 v = make_uint4((s_hist[b * 32u + (lane & 31u)] >> hs) & 0xFFFFu,
+                                         (s_hist[(b + 1) * 32u + (lane & 31u)] >> hs) & 0xFFFFu,
+                                         (s_hist[(b + 2) * 32u + (lane & 31u)] >> hs) & 0xFFFFu,
+                                         (s_hist[(b + 3) * 32u + (lane & 31u)] >> hs) & 0xFFFFu);
+                    if (flushed) {
+                        const uint4 o = ho[b / 4];
+                        v = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
+                    }
+                    ho[b / 4] = v;
+                }
+            }
+#pragma unroll 8
+            for (uint32_t b = 0; b < 256; b += 2) s_hist[b * 32u + lane] = 0;
+            flushed = true;
+        };
+        // block b uses dwords q[16 b .. 16 b + 16]; the loads are clamped to
+        // lastq near the end (bytes from past it are masked off below)
+        auto load16 = [&](uint64_t b, uint32_t (&x)[16]) {
+            const uint64_t base = 16u * b + 1u;
+            if (base + 15u <= lastq) {
+                const uint32_t *qb = q + base;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) dw[k] = nx[k];
-            qb += 16;
-            if (blk + 1 < nfull) load16(qb, blk + 2 == nfull, nx);
+                for (int k = 0; k < 16; ++k) x[k] = qb[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) x[k] = q[min<uint64_t>(base + k, lastq)];
+            }
+        };
+        uint32_t lo = 0, nx[16];
+        if (n) {
+            lo = q[0];
+            load16(0, nx);
+        }
+        for (uint64_t it = 0; it < NB; ++it) {
+            uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                w[k] = __builtin_amdgcn_perm(dw[k], lo, sel);
-                lo = dw[k];
-                count(w[k], 4);
+                w[k] = __builtin_amdgcn_perm(nx[k], lo, sel);
+                lo = nx[k];
             }
-            sha256_block(h, w);
-        }
-    }
-    // the last 1 or 2 blocks: the remaining r < 64 bytes, 0x80, zeros, bit length
-    const uint64_t r = n - nfull * 64u;
-    const uint8_t *tail = p + nfull * 64u;
-    const uint32_t nfin = r <= 55u ? 1u : 2u;
-    for (uint32_t fb = 0; fb < nfin; ++fb) {
+            if (n && it + 1 < nb) load16(it + 1, nx);  // next block's words, in flight during this one
+            const int64_t rb64 = int64_t(n) - int64_t(64u * it);  // bytes of the chunk from this block on
+            const int32_t rb = int32_t(max<int64_t>(-128, min<int64_t>(128, rb64)));
+            if (HIST && rb >= 64) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            uint32_t word = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint64_t pos = uint64_t(fb) * 64u + uint64_t(k) * 4u + j;
-                uint32_t byte = 0;
-                if (pos < r) byte = tail[pos];
-                else if (pos == r) byte = 0x80u;
-                word |= byte << (24u - 8u * j);
+                for (int k = 0; k < 16; ++k) {
+                    count1(w[k] >> 24);
+                    count1(__builtin_amdgcn_ubfe(w[k], 16, 8));
+                    count1(__builtin_amdgcn_ubfe(w[k], 8, 8));
+                    count1(w[k] & 0xFFu);
+                }
             }
-            const uint64_t kpos = uint64_t(fb) * 64u + uint64_t(k) * 4u;
-            if (kpos < r) count(word, uint32_t(min<uint64_t>(4u, r - kpos)));
-            w[k] = word;
+            if (rb < 64 && rb > -64) {  // the lane's final block or two: data bytes, 0x80, zeros, bit length
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int32_t rem = rb - 4 * k;
+                    const uint32_t keep = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * rem));
+                    const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
+                    w[k] = (w[k] & keep) | pad;
+                    if (HIST) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (j < rem) count1((w[k] >> (24 - 8 * j)) & 0xFFu);
+                    }
+                }
+                if (rb <= 55) {
+                    const uint64_t bits = n * 8u;
+                    w[14] = uint32_t(bits >> 32);
+                    w[15] = uint32_t(bits);
+                }
+            }
+            uint4 *st = ring + (it & 1u) * 1024u + lane;
+#pragma unroll
+            for (int k = 0; k < 16; k += 4) st[k * 16] = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+            uint32_t x4[4];
+#pragma unroll
+            for (int t = 16; t < 64; ++t) {
+                const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                const uint32_t wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+                w[t & 15] = wt;
+                x4[t & 3] = wt;
+                if ((t & 3) == 3) st[(t / 4) * 64] = make_uint4(x4[0], x4[1], x4[2], x4[3]);
+            }
+            if (HIST && (it + 1) % kFlushBlocks == 0) flush();
+            __syncthreads();
         }
-        if (fb + 1 == nfin) {
-            const uint64_t bits = n * 8u;
-            w[14] = uint32_t(bits >> 32);
-            w[15] = uint32_t(bits);
+        __syncthreads();  // the consumer's last block
+        if (HIST) flush();
+    } else {
+        uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                         0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+        __syncthreads();  // stage 0 filled
+        for (uint64_t it = 0; it < NB; ++it) {
+            const uint4 *st = ring + (it & 1u) * 1024u + lane;
+            uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+            for (int q4 = 0; q4 < 16; ++q4) {
+                const uint4 v = st[q4 * 64];
+                const uint32_t wq[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = 4 * q4 + j;
+                    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+                    const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+                    const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wq[j];
+                    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+                    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+                    hh = g;
+                    g = f;
+                    f = e;
+                    e = d + t1;
+                    d = c;
+                    c = b;
+                    b = a;
+                    a = t1 + S0 + mj;
+                }
+            }
+            if (it < nb) {
+                h[0] += a;
+                h[1] += b;
+                h[2] += c;
+                h[3] += d;
+                h[4] += e;
+                h[5] += f;
+                h[6] += g;
+                h[7] += hh;
+            }
+            __syncthreads();
         }
-        sha256_block(h, w);
-    }
-    uint4 *out = reinterpret_cast<uint4 *>(digests + i * 32u);
-    auto bswap = [](uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); };
-    out[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
-    out[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
-    if (HIST) {
-        uint4 *ho = reinterpret_cast<uint4 *>(hist + i * 256u);
-#pragma unroll 4
-        for (uint32_t b = 0; b < 256; b += 4)
-            ho[b / 4] = make_uint4(s_hist[b * 64u + lane], s_hist[(b + 1) * 64u + lane], s_hist[(b + 2) * 64u + lane],
-                                   s_hist[(b + 3) * 64u + lane]);
+        if (valid) {
+            uint4 *out = reinterpret_cast<uint4 *>(B.digests + i * 32u);
+            auto bswap = [](uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); };
+            out[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+            out[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+        }
     }
 }
 
@@ -211,11 +261,11 @@ int launch_digests(const DigestBatch &DB, void *stream)
     }
     if (cap == 0 || DB.nbufs == 0) return CDC_OK;
     if ((cap + 63) / 64 > 0x7FFFFFFFull) return CDC_E_INVALID;
-    const dim3 grid(uint32_t((cap + 63) / 64), DB.nbufs), block(64);
+    const dim3 grid(uint32_t((cap + 63) / 64), DB.nbufs), block(128);
     if (hist)
-        hipLaunchKernelGGL(k_chunk_digest<true>, grid, block, kDigestHistBytes, st, DB);
+        hipLaunchKernelGGL(k_chunk_digest<true>, grid, block, kRingBytes + kHistPairBytes, st, DB);
     else
-        hipLaunchKernelGGL(k_chunk_digest<false>, grid, block, 0, st, DB);
+        hipLaunchKernelGGL(k_chunk_digest<false>, grid, block, kRingBytes, st, DB);
     return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
 }
 
