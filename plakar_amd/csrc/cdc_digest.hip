@@ -37,15 +37,16 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU
 }
 
-// Two waves per workgroup of 64 chunks, one lane per chunk in each:
+// Two or three waves per workgroup of 64 chunks, one lane per chunk in each:
 //   wave 1, the producer: loads block b + 1's words while it works on block b,
 //     builds the big-endian words (v_perm funnel shift + byte swap), pads the
-//     final block(s), counts the histogram, and expands the message schedule
-//     W[0..63] into an LDS ring stage;
+//     final block(s) and expands the message schedule W[0..63] into an LDS
+//     ring stage;
+//   wave 2 (histograms requested): the same words, counted;
 //   wave 0, the consumer: the 64 rounds of block b - 1 from the other stage.
 // One s_barrier per block.  The consumer's chain is ~14 VALU per round
-// instead of ~25 when one lane did everything; the producer's ~700 VALU fit
-// under it on another SIMD.
+// instead of ~25 when one lane did everything; the producer's ~560 VALU and
+// the counter's ~160 VALU + 64 LDS atomics fit under it on other SIMDs.
 constexpr uint32_t kShaRing = 2;                                   // stages
 constexpr uint32_t kRingBytes = kShaRing * 64u * 64u * 4u;         // 32 KiB: [stage][word quad][lane] uint4
 // The histogram: u16 halves, lanes l and l + 32 share the dword of bin b at
@@ -63,14 +64,14 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 }
 
 template <bool HIST>
-__global__ __launch_bounds__(128) void k_chunk_digest(const DigestBatch DB)
+__global__ __launch_bounds__(192) void k_chunk_digest(const DigestBatch DB)
 {
     extern __shared__ uint4 s_mem[];
     uint4 *ring = s_mem;                                                   // [kShaRing][16][64]
     uint32_t *s_hist = reinterpret_cast<uint32_t *>(s_mem + kShaRing * 16 * 64);  // [256][32]
     const DigestBuf &B = DB.b[blockIdx.y];
     const uint32_t lane = threadIdx.x & 63u;
-    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
+    const uint32_t role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 rounds, 1 schedule, 2 histogram
     uint64_t n_cuts = B.cap;
     if (B.res) n_cuts = min<uint64_t>(B.cap, uint64_t(B.res->ncuts));
     if (uint64_t(blockIdx.x) * 64u >= n_cuts) return;  // whole workgroup: no barrier is left waiting
@@ -88,14 +89,15 @@ __global__ __launch_bounds__(128) void k_chunk_digest(const DigestBatch DB)
     const uint64_t nb = valid ? n / 64u + ((n % 64u) <= 55u ? 1u : 2u) : 0u;
     const uint64_t NB = wave_max(uint32_t(min<uint64_t>(nb, 0xFFFFFFFFull)));  // both waves: same lanes, same bound
 
-    if (producer) {
+    if (role != 0) {
+        const bool counting = HIST && role == 2;  // uniform per wave
         const uint8_t *p = B.data + (valid ? off : 0);
         const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
         const uint32_t sel = (sh << 24) | ((sh + 1u) << 16) | ((sh + 2u) << 8) | (sh + 3u);
         const uint32_t *q = reinterpret_cast<const uint32_t *>(p - sh);
         const uint64_t lastq = n ? (sh + n - 1u) >> 2 : 0;  // last dword holding a byte of the chunk
         const uint32_t hoff = (lane & 31u) * 4u, hinc = 1u << (16u * (lane >> 5));
-        if (HIST) {
+        if (counting) {
 #pragma unroll 8
             for (uint32_t b = 0; b < 256; b += 2) s_hist[b * 32u + lane] = 0;  // 64 lanes, two bins a step
         }
@@ -153,7 +155,7 @@ __global__ __launch_bounds__(128) void k_chunk_digest(const DigestBatch DB)
             if (n && it + 1 < nb) load16(it + 1, nx);  // next block's words, in flight during this one
             const int64_t rb64 = int64_t(n) - int64_t(64u * it);  // bytes of the chunk from this block on
             const int32_t rb = int32_t(max<int64_t>(-128, min<int64_t>(128, rb64)));
-            if (HIST && rb >= 64) {
+            if (counting && rb >= 64) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
                     count1(w[k] >> 24);
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(128) void k_chunk_digest(const DigestBatch DB)
                     const uint32_t keep = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * rem));
                     const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
                     w[k] = (w[k] & keep) | pad;
-                    if (HIST) {
+                    if (counting) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
                             if (j < rem) count1((w[k] >> (24 - 8 * j)) & 0xFFu);
@@ -181,28 +183,31 @@ __global__ __launch_bounds__(128) void k_chunk_digest(const DigestBatch DB)
                     w[15] = uint32_t(bits);
                 }
             }
-            uint4 *st = ring + (it & 1u) * 1024u + lane;
+            if (!counting) {
+                uint4 *st = ring + (it & 1u) * 1024u + lane;
 #pragma unroll
-            for (int k = 0; k < 16; k += 4) st[k * 16] = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
-            uint32_t x4[4];
+                for (int k = 0; k < 16; k += 4) st[k * 16] = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+                uint32_t x4[4];
 #pragma unroll
-            for (int t = 16; t < 64; ++t) {
-                const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-                const uint32_t wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
-                w[t & 15] = wt;
-                x4[t & 3] = wt;
-                if ((t & 3) == 3) st[(t / 4) * 64] = make_uint4(x4[0], x4[1], x4[2], x4[3]);
+                for (int t = 16; t < 64; ++t) {
+                    const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+                    const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                    const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                    const uint32_t wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+                    w[t & 15] = wt;
+                    x4[t & 3] = wt;
+                    if ((t & 3) == 3) st[(t / 4) * 64] = make_uint4(x4[0], x4[1], x4[2], x4[3]);
+                }
             }
-            if (HIST && (it + 1) % kFlushBlocks == 0) flush();
+            if (counting && (it + 1) % kFlushBlocks == 0) flush();
             __syncthreads();
         }
         __syncthreads();  // the consumer's last block
-        if (HIST) flush();
+        if (counting) flush();
     } else {
         uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+        __builtin_amdgcn_s_setprio(3);  // the critical chain wins issue when waves share a SIMD
         __syncthreads();  // stage 0 filled
         for (uint64_t it = 0; it < NB; ++it) {
             const uint4 *st = ring + (it & 1u) * 1024u + lane;
@@ -261,7 +266,7 @@ int launch_digests(const DigestBatch &DB, void *stream)
     }
     if (cap == 0 || DB.nbufs == 0) return CDC_OK;
     if ((cap + 63) / 64 > 0x7FFFFFFFull) return CDC_E_INVALID;
-    const dim3 grid(uint32_t((cap + 63) / 64), DB.nbufs), block(128);
+    const dim3 grid(uint32_t((cap + 63) / 64), DB.nbufs), block(hist ? 192 : 128);
     if (hist)
         hipLaunchKernelGGL(k_chunk_digest<true>, grid, block, kRingBytes + kHistPairBytes, st, DB);
     else
