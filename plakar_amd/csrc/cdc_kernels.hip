@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "cdc_internal.h"
@@ -231,6 +232,12 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 #ifndef CDC_SCAN_PAIRS
 #define CDC_SCAN_PAIRS 1
 #endif
+#ifndef CDC_EARLY_ISSUE
+#define CDC_EARLY_ISSUE 1
+#endif
+#ifndef CDC_SCAN_V2
+#define CDC_SCAN_V2 1
+#endif
 
 constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
 constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
@@ -323,6 +330,13 @@ __device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, con
     }
 }
 
+__device__ __forceinline__ uint32_t scan_wave_max(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = max(v, uint32_t(__shfl_xor(int(v), o)));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
 // Each lane keeps its run's index record in a register (count + the first
 // kRunCap offsets, see cdc_internal.h) and stores it after its last stage:
 // one coalesced 8-byte store per run, no atomics.
@@ -398,6 +412,115 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     const uint64_t limw = hi_ok - 16u - base;                // last in-bounds piece (lane 0 is in bounds)
     const uint32_t lim = limw > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(limw);
     const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kNBuf * kStageBytes;
+#if CDC_SCAN_V2
+    // Pair staging (see the note below for the 8 runs x 128 B DMA shape) with
+    // a register ping-pong instead of copies: even stages roll from A, odd
+    // stages from Bv.  The half that loads at stage u (u & 1) reads its 128-B
+    // row once, the first 64 B into stage u's array and the second 64 B into
+    // the other array (stage u + 1's); the other half reads nothing.  The DMA
+    // base advances in SGPRs (per-lane offsets fixed); only a wave whose
+    // pieces could leave the buffer takes the clamped form.
+    static_assert(kStage == 64 && kL == 4 && kNBuf == 1, "v2 staging: 64-B stages, one slot");
+    const uint32_t half = lane >> 5;
+    const uint32_t row = lane & 31u, swz = (row >> 1) & 7u;
+    uint32_t off0[4], off1[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t r = 8u * j + lane / 8u;
+        const uint32_t k = (lane % 8u) ^ ((r >> 1) & 7u);
+        off0[j] = uint32_t((((ub + (seg0 + r) * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
+        off1[j] = uint32_t((((ub + (seg0 + 32u + r) * sl) & ~15ull) - kLead + 16u * k) - base);
+    }
+    const uint64_t om0 = scan_wave_max(max(max(off0[0], off0[1]), max(off0[2], off0[3])));
+    const uint64_t om1 = scan_wave_max(max(max(off1[0], off1[1]), max(off1[2], off1[3])));
+    auto issue = [&](auto PC, uint32_t u) {
+        constexpr uint32_t Q = decltype(PC)::value;  // u & 1: the half this DMA feeds
+        const uint32_t (&off)[4] = Q ? off1 : off0;
+        const uint64_t adv = uint64_t(kStage) * (u - Q);
+        if ((Q ? om1 : om0) + adv <= uint64_t(lim)) {
+            dma_stage(base + adv, ring, off);
+        } else {
+            uint32_t eff[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) eff[j] = min(off[j] + uint32_t(adv), lim);
+            dma_stage(base, ring, eff);
+        }
+    };
+    const char *rowp = s_lds + kGearLdsBytes + wave * kStageBytes + row * 128u;
+    auto load_row = [&](uint4 (&first)[4], uint4 (&second)[4]) {
+#pragma unroll
+        for (uint32_t g = 0; g < 4; ++g) first[g] = *reinterpret_cast<const uint4 *>(rowp + 16u * (g ^ swz));
+#pragma unroll
+        for (uint32_t g = 0; g < 4; ++g) second[g] = *reinterpret_cast<const uint4 *>(rowp + 16u * ((g + 4) ^ swz));
+    };
+    const uint32_t TT = T + 1;  // half 1 runs one stage behind
+    const int32_t lag = int32_t(kStage * half);
+    const uint32_t vhi = to_vgpr(P.fs_hi);
+    const uint32_t xlo = P.fs_lo, xhi = P.fs_hi;
+    const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
+    using C0 = std::integral_constant<uint32_t, 0>;
+    using C1 = std::integral_constant<uint32_t, 1>;
+
+    uint4 A[4] = {}, Bv[4] = {};  // half 1's stage-0 bytes are warm-up: zeros
+    issue(C0{}, 0);
+    wait_vmcnt<0>();
+    if (half == 0) load_row(A, Bv);
+    if (1 < TT) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(C1{}, 1);
+    }
+    uint64_t gv[2][16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(A[0], k >> 2), k));
+    uint64_t fp = 0;
+    uint64_t rec = 0;
+    const int32_t len = int32_t(e - s);
+    const int32_t rr0 = int32_t(rel0 - s) - lag;
+    // One stage t of parity Q: rolls cur (stage t's data); at its last group
+    // the half loading stage t + 1 fills nxt (stage t + 1) and cur (t + 2),
+    // and once those reads retired the slot takes DMA t + 2.
+    auto stage = [&](auto PC, uint32_t t, uint4 (&cur_d)[4], uint4 (&nxt_d)[4]) {
+        constexpr uint32_t Q = decltype(PC)::value;
+#pragma unroll
+        for (uint32_t gi = 0; gi < kGroups; ++gi) {
+            if (gi + 1 == kGroups && t + 1 < TT) {
+                wait_vmcnt<0>();  // DMA t + 1 landed
+                if (half != Q) load_row(nxt_d, cur_d);
+                asm volatile("" ::: "memory");
+            }
+            const uint4 nx = gi + 1 < kGroups ? cur_d[gi + 1] : nxt_d[0];
+            uint64_t (&cg)[16] = gv[gi & 1];
+            uint64_t (&ng)[16] = gv[(gi + 1) & 1];
+            const uint64_t f0 = fp;
+            uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int k = 4 * q; k < 4 * q + 4; k += 2) {
+                    fp = (fp << 1) + cg[k];
+                    const uint32_t k0 = uint32_t(fp >> 32) & vhi;
+                    fp = (fp << 1) + cg[k + 1];
+                    acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 4 * q; k < 4 * q + 4; ++k) ng[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
+                __builtin_amdgcn_sched_barrier(0);
+                if (q == 1 && gi + 1 == kGroups && t + 2 < TT) {
+                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the row reads precede these 8 gathers
+                    issue(PC, t + 2);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (acc == 0) [[unlikely]]
+                recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
+        }
+    };
+    for (uint32_t t = 0; t < TT; t += 2) {
+        stage(C0{}, t, A, Bv);
+        if (t + 1 < TT) stage(C1{}, t + 1, Bv, A);
+    }
+#else
 #if CDC_SCAN_PAIRS
     // Pair staging: DMA t carries 128 B (whole lines) of each of the 32 runs
     // of half t & 1 of the wave (4 instructions of 8 runs x 128 B), which reads
@@ -496,6 +619,15 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     uint4 d[kGroups];
     load_stage(0, d);
     asm volatile("" ::: "memory");  // the slot reads issue before any gather (see the lgkmcnt below)
+#if CDC_EARLY_ISSUE
+    // Early issue: a slot is refilled as soon as the wave's own reads of it
+    // have retired (LDS-DMA does not wait for earlier ds_reads; the counted
+    // lgkmcnt does), so stage t + kNBuf is in flight for ~3.5 groups instead of 2.
+    if (kNBuf < TT) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(kNBuf);
+    }
+#endif
     // gathers double-buffered by group parity: group gi rolls gv[gi & 1] while
     // the next group's values land in gv[(gi + 1) & 1]; a recheck reads the
     // rolled group's values from registers.
@@ -514,7 +646,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
         uint4 dn[kGroups];
 #pragma unroll
         for (uint32_t gi = 0; gi < kGroups; ++gi) {
-            if (gi == 1 && t + kNBuf < TT) {
+            if (!CDC_EARLY_ISSUE && gi == 1 && t + kNBuf < TT) {
                 // >= 16 gathers were issued after stage t's slot reads: lgkmcnt(15)
                 // retires those reads, and the slot can take stage t + kNBuf.
                 asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
@@ -555,6 +687,14 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
 #pragma unroll
                 for (int k = 4 * q; k < 4 * q + 4; ++k) nxt[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
                 __builtin_amdgcn_sched_barrier(0);
+#if CDC_EARLY_ISSUE
+                if (q == 1 && gi + 1 == kGroups && t + 1 + kNBuf < TT) {
+                    // the slot reads of load_stage(t + 1) precede these 8 gathers
+                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                    issue(t + 1 + kNBuf);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#endif
             }
 #if CDC_DIAG_NO_RECHECK
             if (acc == 0x12345) [[unlikely]]
@@ -575,6 +715,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
 #pragma unroll
         for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
     }
+#endif
     if (s < int64_t(D.len)) W.runs[64ull * D.task_base + seg0 + lane] = rec;
     if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
