@@ -238,6 +238,9 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 #ifndef CDC_SCAN_V2
 #define CDC_SCAN_V2 1
 #endif
+#ifndef CDC_TAIL_PRIO
+#define CDC_TAIL_PRIO 3
+#endif
 
 constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
 constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
@@ -491,6 +494,15 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
             const uint4 nx = gi + 1 < kGroups ? cur_d[gi + 1] : nxt_d[0];
             uint64_t (&cg)[16] = gv[gi & 1];
             uint64_t (&ng)[16] = gv[(gi + 1) & 1];
+#if CDC_DIAG_NO_COMPUTE
+            fp += nx.x ^ cur_d[gi].w;  // diagnostic: staging only
+            if (fp == 0x123456789ull) rec = fp;
+            if (gi + 1 == kGroups && t + 2 < TT) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                issue(PC, t + 2);
+            }
+            continue;
+#endif
             const uint64_t f0 = fp;
             uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
@@ -512,7 +524,11 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+#if CDC_DIAG_NO_RECHECK
+            if (acc == 0x12345) [[unlikely]]
+#else
             if (acc == 0) [[unlikely]]
+#endif
                 recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
         }
     };
@@ -1210,7 +1226,7 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
 __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(const Batch B, const DevParams P,
                                                                const Workspace W)
 {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
 #if CDC_WALK_SPEC
     __shared__ uint64_t s_prec[kWalkWavesPerWG][kPreRuns];
@@ -1292,7 +1308,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
 __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk2(const Batch B, const DevParams P,
                                                                const Workspace W)
 {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     const bool l0 = (threadIdx.x & 63u) == 0;
@@ -1386,7 +1402,7 @@ constexpr uint32_t kSeqThreads = 256;
 
 __global__ __launch_bounds__(kSeqThreads) CDC_WALK_ATTR void k_seq(const Batch B, const DevParams P, const Workspace W)
 {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
     const uint32_t b = blockIdx.x;
     if (!B.force_fallback && W.flags[b] == 0) return;
@@ -1458,7 +1474,7 @@ __host__ __device__ inline uint32_t emit_wgs(uint32_t nseg)
 // one wave per segment with lane i writing cut i (coalesced).
 __global__ __launch_bounds__(kEmitThreads) void k_emit(const Batch B, const DevParams P, const Workspace W)
 {
-    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     // u16 lists (segment indices < kMaxSegs; kConv* sentinels kept in the top
     // three codes) so that an emit workgroup fits beside a scan workgroup.
     __shared__ uint16_t s_nt[kNtCap];
@@ -1760,6 +1776,19 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         hipExtLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
     } else {
         hipLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, B, P, W);
+    }
+    // diagnostic (CDC_DIAG_SCAN_ONLY=1): the scan alone, no resolution (cut lists not written)
+    static const bool scan_only = [] {
+        const char *e = getenv("CDC_DIAG_SCAN_ONLY");
+        return e && e[0] == '1';
+    }();
+    if (scan_only) {
+        if (prof) {
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            (void)hipEventRecord(pr.e2, st);
+            g_prof_live.push_back(pr);
+        }
+        return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
     }
     if (B.total_segs > 0 && !B.force_fallback) {
         const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
