@@ -11,13 +11,16 @@ chunk_digests() runs the HIP kernel of libplakar_cdc.so
 (cdc_chunk_digests_device_async): one SHA-256 and one 256-bin histogram per
 chunk of a device cut list.  The float64 entropy is computed here, on the host,
 with the reference's formula and summation order, from the exact integer
-histogram.
+histogram, with Go's math.Log2 restated (go_log2: math/log2.go's frexp
+split over the fdlibm log that math/log.go implements).  Go is not available
+here, so bit-identity with Go's floats is unpinned.
 """
 import ctypes
 import math
 from dataclasses import dataclass, field
 from typing import List
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -99,9 +102,89 @@ def chunk_digests_batch(datas, cut_lists, results=None, hist=True, stream=None):
     return outs
 
 
+# --------------------------------------------------------------------- Go Log2
+# fdlibm e_log.c constants (Go math/log.go uses the same algorithm)
+_LN2_HI = 6.93147180369123816490e-01
+_LN2_LO = 1.90821492927058770002e-10
+_LG = (6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01,
+       2.222219843214978396e-01, 1.818357216161805012e-01, 1.531383769920937332e-01,
+       1.479819860511658591e-01)
+_SQRT2_2 = math.sqrt(2.0) / 2.0
+_INV_LN2 = float.fromhex("0x1.71547652b82fep+0")  # Go constant 1/Ln2, rounded once
+
+
+def _go_log_reduced(f1, ki):
+    """Go's log(x) for x = f1 * 2**ki, f1 in [0.5, 1) (frexp form), x > 0 finite."""
+    if f1 < _SQRT2_2:
+        f1 *= 2.0
+        ki -= 1
+    f = f1 - 1.0
+    k = float(ki)
+    s = f / (2.0 + f)
+    s2 = s * s
+    s4 = s2 * s2
+    t1 = s2 * (_LG[0] + s4 * (_LG[2] + s4 * (_LG[4] + s4 * _LG[6])))
+    t2 = s4 * (_LG[1] + s4 * (_LG[3] + s4 * _LG[5]))
+    r = t1 + t2
+    hfsq = 0.5 * f * f
+    return k * _LN2_HI - ((hfsq - (s * (hfsq + r) + k * _LN2_LO)) - f)
+
+
+def go_log2(x):
+    """math.Log2 as Go defines it for finite x > 0: frac, exp := Frexp(x);
+    frac == 0.5 -> exp - 1; else Log(frac) * (1/Ln2) + exp."""
+    frac, exp = math.frexp(x)
+    if frac == 0.5:
+        return float(exp - 1)
+    return _go_log_reduced(*math.frexp(frac)) * _INV_LN2 + float(exp)
+
+
+def go_log2_array(x):
+    """go_log2 over a float64 array (elementwise IEEE operations in the same
+    order; numpy ufuncs do not contract into FMAs)."""
+    x = np.asarray(x, dtype=np.float64)
+    frac, exp = np.frexp(x)
+    f1, ki = np.frexp(frac)  # frac in [0.5, 1): f1 == frac, ki == 0
+    small = f1 < _SQRT2_2
+    f1 = np.where(small, f1 * 2.0, f1)
+    k = (ki - small.astype(np.int64)).astype(np.float64)
+    f = f1 - 1.0
+    s = f / (2.0 + f)
+    s2 = s * s
+    s4 = s2 * s2
+    t1 = s2 * (_LG[0] + s4 * (_LG[2] + s4 * (_LG[4] + s4 * _LG[6])))
+    t2 = s4 * (_LG[1] + s4 * (_LG[3] + s4 * _LG[5]))
+    r = t1 + t2
+    hfsq = 0.5 * f * f
+    lg = k * _LN2_HI - ((hfsq - (s * (hfsq + r) + k * _LN2_LO)) - f)
+    out = lg * _INV_LN2 + exp.astype(np.float64)
+    return np.where(frac == 0.5, (exp - 1).astype(np.float64), out)
+
+
+def entropy_rows(hist, lengths):
+    """entropy() of backup.go:548-569 for every row of an integer histogram
+    (n, 256) with row sums `lengths`: -sum_b p_b log2 p_b over the bins with
+    p_b > 0, accumulated left to right.  Returns float64 (n,)."""
+    hist = np.asarray(hist, dtype=np.float64)
+    lengths = np.asarray(lengths, dtype=np.float64)
+    n = hist.shape[0]
+    out = np.zeros(n, dtype=np.float64)
+    nz = lengths > 0
+    if not nz.any():
+        return out
+    h = hist[nz]
+    p = h / lengths[nz, None]
+    pos = h > 0
+    terms = np.zeros_like(p)
+    terms[pos] = p[pos] * go_log2_array(p[pos])
+    # e = 0; e -= t_0; e -= t_1; ...  == cumulative sum of -t, in bin order
+    out[nz] = np.cumsum(-terms, axis=1)[:, -1]
+    return out
+
+
 def entropy_from_freq(freq, size):
     """entropy() of snapshot/backup.go:548-569 from its frequency table: the
-    same float64 terms in the same order (bins 0..255)."""
+    same float64 terms in the same order (bins 0..255), with Go's Log2."""
     if size == 0:
         return 0.0
     e = 0.0
@@ -109,7 +192,7 @@ def entropy_from_freq(freq, size):
     for f in freq:
         if f > 0:
             p = float(f) / data_size
-            e -= p * math.log2(p)
+            e -= p * go_log2(p)
     return e
 
 
@@ -140,5 +223,5 @@ def chunk_records(data, cuts, result=None):
 
 
 __all__ = ["Configuration", "LookupDefaultConfiguration", "DefaultConfiguration", "chunk_digests",
-           "chunk_digests_batch",
+           "chunk_digests_batch", "go_log2", "go_log2_array", "entropy_rows",
            "entropy_from_freq", "Chunk", "chunk_records", "_lib"]

@@ -1,0 +1,162 @@
+"""Batched chunkify: plakar's per-file chunking work for a batch of whole
+in-memory files, on the device.
+
+    snapshot/backup.go:631-666   routing: empty file -> one empty chunk; smaller
+                                 than Chunking.MinSize -> the whole file, no CDC;
+                                 otherwise the chunker's cuts
+    snapshot/backup.go:594-629   processChunk: chunk SHA-256, entropy() and the
+                                 normalised byte distribution -> objects.Chunk
+    snapshot/backup.go:668-681   the object's Entropy (length-weighted mean of
+                                 the chunk entropies) and Checksum (SHA-256 of
+                                 the whole file, objectHasher)
+    objects/objects.go:26-36, 73-79   Object / Chunk
+
+This is the batch form that SURVEY.md section 8b proposes for the re-plumbed
+backup: one call per batch of files instead of one chunker per file.  The
+cut points come from the device chunker (libplakar_cdc.so), the chunk
+checksums and byte counts from one batched k_chunk_digest launch group, and
+only the float64 arithmetic runs on the host.
+
+The float64 arithmetic keeps the reference's order (hashing.entropy_rows: bins
+0..255 in sequence, Go's math.Log2 restated; the object entropy summed over
+the chunks in sequence).  Nothing here could be run against Go in this
+container, so the bit-identity of the floats to Go is unpinned; the integer
+parts (cuts, checksums, counts) are exact.
+
+Chunk.Distribution and Object.Distribution are float64 numpy rows of 256
+(the Go [256]float64 arrays).
+
+Out of scope, as in SURVEY.md: the content type (mime detection), the
+classifier, the blob dedup and PutBlob / packer (storage), and the
+object's Distribution (the reference never assigns it from its running
+total: backup.go:668-677 leaves it zero).
+
+The per-object SHA-256 is one serial chain per file.  On the device it is one
+lane per file, ~32 MB/s per lane: it pays for many small files hashed
+together and loses to a host core (~2 GB/s with SHA extensions) on a large
+file.  object_hash="auto" hashes files up to `device_object_max` bytes on the
+device (batched) and the rest with hashlib on host threads, overlapped with
+the device work.
+"""
+import concurrent.futures
+import hashlib
+import warnings
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+import torch
+
+from . import chunkers, device, hashing
+from .repository import Repository
+
+# ------------------------------------------------------------------- records
+@dataclass
+class Object:
+    """objects.Object (objects/objects.go:26-36), the fields chunkify fills."""
+    Checksum: bytes
+    Chunks: List[hashing.Chunk] = field(default_factory=list)
+    ContentType: str = ""
+    Entropy: float = 0.0
+    Distribution: np.ndarray = field(default_factory=lambda: np.zeros(256))
+
+
+def route(size, min_size):
+    """snapshot/backup.go:631-645: 'empty', 'whole' (one chunk, no CDC) or 'cdc'."""
+    if size == 0:
+        return "empty"
+    if size < min_size:
+        return "whole"
+    return "cdc"
+
+
+def _object_entropy(chunk_entropies, lengths):
+    """backup.go:612-627 + 668-670: totalEntropy += e * len (chunk order);
+    Entropy = totalEntropy / totalDataSize."""
+    total = int(np.sum(lengths, dtype=np.uint64))
+    if total == 0:
+        return 0.0
+    acc = np.cumsum(np.asarray(chunk_entropies, np.float64) * np.asarray(lengths, np.float64))[-1]
+    return float(acc) / float(total)
+
+
+def chunkify_batch(files, repo: Repository = None, dev=0, object_hash="auto", device_object_max=1 << 20,
+                   host_threads=8):
+    """chunkify() for a batch of whole files held in host memory (bytes,
+    bytearray or uint8 arrays).  Returns one Object per file, in order."""
+    repo = repo or Repository()
+    cfg = repo.Chunking
+    opts = chunkers.ChunkerOpts(MinSize=int(cfg.MinSize), NormalSize=int(cfg.NormalSize),
+                                MaxSize=int(cfg.MaxSize))
+    chunkers.Validate(cfg.Algorithm.lower(), opts)
+    arrs = [np.frombuffer(f, dtype=np.uint8) if not isinstance(f, np.ndarray) else np.ascontiguousarray(f, np.uint8)
+            for f in files]
+    n = len(arrs)
+    if n == 0:
+        return []
+    routes = [route(a.size, opts.MinSize) for a in arrs]
+    d = torch.device("cuda", dev)
+
+    # per-object SHA-256 of the large files on host threads, overlapped
+    host_obj = [i for i in range(n) if object_hash == "host" or (object_hash == "auto" and arrs[i].size > device_object_max)]
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=max(1, host_threads)) if host_obj else None
+    futs = {i: pool.submit(lambda a: hashlib.sha256(memoryview(a)).digest(), arrs[i]) for i in host_obj}
+
+    with warnings.catch_warnings():  # read-only views of bytes objects: only read here
+        warnings.simplefilter("ignore", UserWarning)
+        tens = [torch.from_numpy(a).to(d) if a.size else torch.empty(0, dtype=torch.uint8, device=d) for a in arrs]
+    # cut lists: device chunker for 'cdc' files, one whole-file cut otherwise
+    cdc_idx = [i for i in range(n) if routes[i] == "cdc"]
+    cuts = [None] * n
+    if cdc_idx:
+        b = device.DeviceBatch([tens[i] for i in cdc_idx], opts)
+        b.launch()
+        got, _ = b.results()
+        for i, c in zip(cdc_idx, got):
+            cuts[i] = c.contiguous()
+    whole_idx = [i for i in range(n) if cuts[i] is None]
+    if whole_idx:  # one host-to-device copy for every whole-file cut
+        rows = torch.tensor([[0, arrs[i].size] for i in whole_idx], dtype=torch.int64).to(d)
+        for k, i in enumerate(whole_idx):
+            cuts[i] = rows[k:k + 1]
+    # every chunk's SHA-256 + byte counts: one batched launch group
+    nonempty = [i for i in range(n) if tens[i].numel() > 0]
+    outs = hashing.chunk_digests_batch([tens[i] for i in nonempty], [cuts[i] for i in nonempty]) if nonempty else []
+    dev_obj = [i for i in nonempty if i not in futs]
+    obj_outs = []
+    if dev_obj:
+        whole = torch.tensor([[0, arrs[i].size] for i in dev_obj], dtype=torch.int64).to(d)
+        obj_outs = hashing.chunk_digests_batch([tens[i] for i in dev_obj], [whole[k:k + 1] for k in range(len(dev_obj))],
+                                               hist=False)
+    # one device-to-host copy of each kind for the whole batch
+    if nonempty:
+        lens_all = torch.cat([cuts[i][:, 1] for i in nonempty]).cpu().numpy().astype(np.int64)
+        dg_all = torch.cat([o[0] for o in outs]).cpu().numpy()
+        hist_all = torch.cat([o[1] for o in outs]).cpu().numpy()
+    obj_all = torch.cat([o[0] for o in obj_outs]).cpu().numpy() if obj_outs else None
+    obj_row = {i: k for k, i in enumerate(dev_obj)}
+    if nonempty:
+        ent_all = hashing.entropy_rows(hist_all, lens_all)
+        dist_all = hist_all.astype(np.float64) / np.maximum(lens_all, 1)[:, None].astype(np.float64)
+
+    empty_sha = hashlib.sha256(b"").digest()
+    objects = []
+    k0 = 0
+    for i in range(n):
+        if arrs[i].size == 0:  # backup.go:631-635: one empty chunk, entropy 0, zero distribution
+            objects.append(Object(Checksum=empty_sha, Chunks=[hashing.Chunk(empty_sha, 0, 0.0, np.zeros(256))]))
+            continue
+        m = cuts[i].shape[0]
+        sl = slice(k0, k0 + m)
+        k0 += m
+        lens, ent = lens_all[sl], ent_all[sl]
+        chunks = [hashing.Chunk(dg_all[k].tobytes(), int(lens_all[k]), float(ent_all[k]), dist_all[k])
+                  for k in range(sl.start, sl.stop)]
+        checksum = futs[i].result() if i in futs else obj_all[obj_row[i]].tobytes()
+        objects.append(Object(Checksum=checksum, Chunks=chunks, Entropy=_object_entropy(ent, lens)))
+    if pool:
+        pool.shutdown()
+    return objects
+
+
+__all__ = ["Object", "route", "chunkify_batch"]

@@ -41,7 +41,8 @@ def test_hashing_configuration_mirror():
 
 
 def _entropy_direct(data):
-    """snapshot/backup.go:548-569 restated over the bytes."""
+    """snapshot/backup.go:548-569 restated over the bytes (Go's Log2)."""
+    from plakar_amd.hashing import go_log2
     if len(data) == 0:
         return 0.0, [0.0] * 256
     freq = [0.0] * 256
@@ -52,7 +53,7 @@ def _entropy_direct(data):
     for f in freq:
         if f > 0:
             p = f / size
-            e -= p * math.log2(p)
+            e -= p * go_log2(p)
     return e, freq
 
 
@@ -64,6 +65,48 @@ def test_entropy_from_histogram_matches_reference_formula():
         hist = np.bincount(data, minlength=256) if n else np.zeros(256, np.int64)
         assert hashing.entropy_from_freq(hist.tolist(), n) == e  # same terms, same order: bit-identical
         assert [float(x) for x in hist] == freq
+
+
+def test_go_log2_restatement():
+    """Go's math.Log2 = frexp split + fdlibm log (math/log2.go, math/log.go):
+    exact at powers of two, within 1 ulp of log2 elsewhere, and the numpy
+    form is bit-identical to the scalar form."""
+    from plakar_amd import hashing
+    for k in range(-40, 41):
+        assert hashing.go_log2(2.0 ** k) == float(k)
+    xs = np.random.default_rng(5).random(50000) + 1e-300
+    v = hashing.go_log2_array(xs)
+    assert np.array_equal(v[:5000], np.array([hashing.go_log2(float(x)) for x in xs[:5000]]))
+    ref = np.log2(xs)
+    assert (np.abs(v - ref) <= np.spacing(np.abs(ref))).all()
+    # fdlibm log itself: within 1 ulp of math.log on the reduced range
+    for x in np.linspace(0.5, 1.0, 1001)[:-1]:
+        f1, ki = math.frexp(float(x))
+        assert abs(hashing._go_log_reduced(f1, ki) - math.log(float(x))) <= 2 * np.spacing(abs(math.log(float(x))) + 1e-300)
+
+
+def test_entropy_rows_matches_scalar():
+    """The vectorised entropy (bins summed left to right with cumsum) is
+    bit-identical to the scalar reference loop, including empty rows,
+    single-valued rows and rows with empty bins."""
+    from plakar_amd import hashing
+    rng = np.random.default_rng(9)
+    rows = [np.zeros(256, np.int64), np.eye(256, dtype=np.int64)[7] * 1000]
+    for n in (1, 2, 3, 100, 4096, 70000):
+        rows.append(np.bincount(rng.integers(0, rng.integers(1, 257), n), minlength=256))
+    hist = np.stack(rows)
+    lens = hist.sum(axis=1)
+    got = hashing.entropy_rows(hist, lens)
+    for i in range(len(rows)):
+        assert got[i] == hashing.entropy_from_freq(hist[i].tolist(), int(lens[i]))
+
+
+def test_chunkify_routing():
+    from plakar_amd import snapshot
+    assert snapshot.route(0, 65536) == "empty"
+    assert snapshot.route(1, 65536) == "whole"
+    assert snapshot.route(65535, 65536) == "whole"
+    assert snapshot.route(65536, 65536) == "cdc"
 
 
 # ------------------------------------------------------------------ GPU parity
@@ -175,3 +218,48 @@ def test_gpu_digest_batch_many_buffers():
     torch.cuda.synchronize()
     for (data, cuts), (d, h) in zip(refs, outs):
         _check(data, cuts, d[:len(cuts)].cpu().numpy(), h[:len(cuts)].cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_gpu_chunkify_batch_objects(oracle):
+    """snapshot.chunkify_batch against the reference's per-file work restated
+    on the CPU: routing (backup.go:631-645), oracle cuts, hashlib chunk and
+    object checksums, exact counts, Go-Log2 entropies, the object entropy as
+    the length-weighted sum in chunk order."""
+    torch = _gpu()
+    from datagen import low_entropy
+    from plakar_amd import _lib, snapshot
+    from plakar_amd.hashing import go_log2
+    _lib.ensure_init(gear=_lib.default_gear())
+    gear = _lib.default_gear()
+    files = [b"", b"x", random_bytes(1000, 50).tobytes(), random_bytes(65535, 51).tobytes(),
+             random_bytes(65536, 52).tobytes(), random_bytes(3 << 20, 53).tobytes(),
+             low_entropy(9 << 20, 54).tobytes(), random_bytes((2 << 20) + 12345, 55).tobytes()]
+    objs = snapshot.chunkify_batch(files, device_object_max=4 << 20)
+    assert len(objs) == len(files)
+    for f, o in zip(files, objs):
+        a = np.frombuffer(f, np.uint8)
+        if a.size == 0:
+            cuts = [(0, 0)]
+        elif a.size < 65536:
+            cuts = [(0, a.size)]
+        else:
+            cuts = [(int(x), int(y)) for x, y in oracle.chunk(a, gear)]
+        assert [c.Length for c in o.Chunks] == [n for _, n in cuts]
+        assert o.Checksum == hashlib.sha256(f).digest()
+        tot_e, tot = 0.0, 0
+        for (off, n), c in zip(cuts, o.Chunks):
+            part = f[off:off + n]
+            assert c.Checksum == hashlib.sha256(part).digest()
+            freq = [float(x) for x in np.bincount(np.frombuffer(part, np.uint8), minlength=256)]
+            e = 0.0
+            for x in freq:  # backup.go:560-566, bins in order
+                if x > 0:
+                    q = x / float(n)
+                    e -= q * go_log2(q)
+            assert c.Entropy == e
+            assert list(c.Distribution) == ([x / n for x in freq] if n else [0.0] * 256)
+            tot_e += c.Entropy * float(n)
+            tot += n
+        assert o.Entropy == (tot_e / float(tot) if tot else 0.0)
+        assert list(o.Distribution) == [0.0] * 256
