@@ -426,26 +426,27 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     static_assert(kStage == 64 && kL == 4 && kNBuf == 1, "v2 staging: 64-B stages, one slot");
     const uint32_t half = lane >> 5;
     const uint32_t row = lane & 31u, swz = (row >> 1) & 7u;
-    uint32_t off0[4], off1[4];
+    // Half 1's runs are 32 runs after half 0's (lane lengths are multiples of
+    // 256 B, so the 16-B alignment commutes): its pieces are half 0's offsets
+    // plus the uniform 32 sl, added to the SGPR base.
+    uint32_t off0[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t r = 8u * j + lane / 8u;
         const uint32_t k = (lane % 8u) ^ ((r >> 1) & 7u);
         off0[j] = uint32_t((((ub + (seg0 + r) * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
-        off1[j] = uint32_t((((ub + (seg0 + 32u + r) * sl) & ~15ull) - kLead + 16u * k) - base);
     }
     const uint64_t om0 = scan_wave_max(max(max(off0[0], off0[1]), max(off0[2], off0[3])));
-    const uint64_t om1 = scan_wave_max(max(max(off1[0], off1[1]), max(off1[2], off1[3])));
+    const uint64_t half_step = 32ull * sl;
     auto issue = [&](auto PC, uint32_t u) {
         constexpr uint32_t Q = decltype(PC)::value;  // u & 1: the half this DMA feeds
-        const uint32_t (&off)[4] = Q ? off1 : off0;
-        const uint64_t adv = uint64_t(kStage) * (u - Q);
-        if ((Q ? om1 : om0) + adv <= uint64_t(lim)) {
-            dma_stage(base + adv, ring, off);
+        const uint64_t adv = uint64_t(kStage) * (u - Q) + (Q ? half_step : 0ull);
+        if (om0 + adv <= uint64_t(lim)) {
+            dma_stage(base + adv, ring, off0);
         } else {
             uint32_t eff[4];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) eff[j] = min(off[j] + uint32_t(adv), lim);
+            for (uint32_t j = 0; j < 4; ++j) eff[j] = min(off0[j] + uint32_t(adv), lim);
             dma_stage(base, ring, eff);
         }
     };
