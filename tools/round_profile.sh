@@ -23,11 +23,11 @@ tail -1 "$OUT/bench_c4.json" | cut -c1-300
 
 echo "[4/5] rocprofv3 kernel trace + stats (c1)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace" -o run -- \
-    python3 bench.py --steps 20 --warmup 3 --streams 1 --no-cpu-baseline --e2e-reps 0 > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.err"
+    python3 bench.py --steps 100 --warmup 200 --streams 1 --no-cpu-baseline --e2e-reps 0 --digest-reps 0 > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.err"
 python tools/kstats.py "$OUT/ktrace/run_kernel_trace.csv" > "$OUT/kernel_summary.txt"; head -10 "$OUT/kernel_summary.txt"
 
 echo "[5/5] rocprofv3 PMC FETCH_SIZE (c1)"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc" -o run -- \
-    python3 bench.py --steps 5 --warmup 1 --streams 1 --no-cpu-baseline --e2e-reps 0 > "$OUT/pmc_bench.json" 2> "$OUT/pmc.err"
+    python3 bench.py --steps 5 --warmup 1 --streams 1 --no-cpu-baseline --e2e-reps 0 --digest-reps 0 > "$OUT/pmc_bench.json" 2> "$OUT/pmc.err"
 python tools/pmc_summary.py "$OUT/pmc" k_scan | tee "$OUT/pmc_summary.txt"
 echo done
