@@ -1665,7 +1665,11 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 {
     uint64_t maxlen = 0;
     for (int i = 0; i < nbufs; ++i) maxlen = lens[i] > maxlen ? lens[i] : maxlen;
-    uint64_t mult = 16;
+    // Resolution segments of 32 Min (2 MiB at the default sizes): fewer,
+    // longer speculative walks occupy fewer CUs beside the next pass's scan
+    // (C1 pipelined: 16 Min 4.47-4.52k GiB/s, 24 4.64k, 32 4.67-4.70k, 48
+    // 4.52k, 64 4.40k; single-pass latency 0.255 -> 0.266 ms).
+    uint64_t mult = 32;
     if (const char *env = getenv("CDC_SEG_MULT")) {
         const long v = atol(env);
         if (v >= 2 && v <= 1024) mult = uint64_t(v);
