@@ -21,7 +21,10 @@ constexpr uint32_t kRunCap = 3;
 constexpr uint32_t kMaxScanLane = 65536;  // run offsets are u16
 constexpr uint32_t kMaxSegs = 16384;    // resolution segments per buffer
 constexpr uint32_t kScanLaneBytes = 16384;  // max bytes hashed+tested per scan lane (multiple of 256)
-constexpr uint32_t kWalkWavesPerWG = 4;   // latency-bound walkers: registers over occupancy
+#ifndef CDC_WALK_WAVES
+#define CDC_WALK_WAVES 4
+#endif
+constexpr uint32_t kWalkWavesPerWG = CDC_WALK_WAVES;   // latency-bound walkers: registers over occupancy
 constexpr uint64_t kUndet = ~0ull;      // "next chunk start not decided by the bytes present"
 
 // Chunker parameters as the kernels use them.

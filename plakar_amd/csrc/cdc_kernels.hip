@@ -465,17 +465,25 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     using C0 = std::integral_constant<uint32_t, 0>;
     using C1 = std::integral_constant<uint32_t, 1>;
 
-    uint4 A[4] = {}, Bv[4] = {};  // half 1's stage-0 bytes are warm-up: zeros
+    uint4 A[4] = {}, Bv[4] = {};
+    // Stage 0 is not rolled: it lies 128 B (half 0) or 192 B (half 1) before
+    // the run, and stage 1 alone gives fp >= 64 >= W - 1 warm-up bytes.  Its
+    // loads and DMA issues are kept.
+    static_assert(kLead >= 2 * kStage, "stage 0 must be pure warm-up for both halves");
     issue(C0{}, 0);
     wait_vmcnt<0>();
-    if (half == 0) load_row(A, Bv);
+    if (half == 0) load_row(A, Bv);  // stage 0 (unused) and stage 1 of half 0
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (1 < TT) issue(C1{}, 1);
     if (1 < TT) {
+        wait_vmcnt<0>();
+        if (half == 1) load_row(Bv, A);  // stages 1 and 2 of half 1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue(C1{}, 1);
+        if (2 < TT) issue(C0{}, 2);
     }
     uint64_t gv[2][16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(A[0], k >> 2), k));
+    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(Bv[0], k >> 2), k));
     uint64_t fp = 0;
     uint64_t rec = 0;
     const int32_t len = int32_t(e - s);
@@ -533,7 +541,8 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
                 recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
         }
     };
-    for (uint32_t t = 0; t < TT; t += 2) {
+    if (1 < TT) stage(C1{}, 1, Bv, A);
+    for (uint32_t t = 2; t < TT; t += 2) {
         stage(C0{}, t, A, Bv);
         if (t + 1 < TT) stage(C1{}, t + 1, Bv, A);
     }
