@@ -39,7 +39,10 @@
 namespace cdc {
 
 static constexpr uint64_t kNoHit = ~0ull;
-static constexpr uint32_t kRawLaneBytes = 256;  // bytes tested per lane per raw-scan block
+#ifndef CDC_RAW_LANE
+#define CDC_RAW_LANE 256
+#endif
+static constexpr uint32_t kRawLaneBytes = CDC_RAW_LANE;  // bytes tested per lane per raw-scan block
 static constexpr uint32_t kWarm = 64;           // warm-up bytes (>= W - 1 for any mask)
 static constexpr uint32_t kNtCap = 4096;        // emit: non-trivial junctions per buffer
 
@@ -84,8 +87,15 @@ __device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gea
 #else
 #define CDC_WALK_ATTR
 #endif
-constexpr uint32_t kWCopies = 8;    // walker table copies
-constexpr uint32_t kWEntShift = 6;  // log2(kWCopies * 8): bytes per walker table entry
+// Walker table copies: 8 by default (16 KiB).  32 (the scan's layout:
+// conflict-free gathers, one-instruction v_perm address) made C3's raw MaskL
+// scans 3.5 % faster but C1 2 % slower (a 64-KiB fill per walker workgroup).
+#ifndef CDC_WALK_COPIES
+#define CDC_WALK_COPIES 8
+#endif
+constexpr uint32_t kWCopies = CDC_WALK_COPIES;
+constexpr uint32_t kWEntShift = kWCopies == 32 ? 8 : kWCopies == 16 ? 7 : 6;  // log2(kWCopies * 8)
+static_assert(kWCopies == 8 || kWCopies == 16 || kWCopies == 32, "walker table copies");
 
 __device__ __forceinline__ uint64_t lds_gear(const char *tab, uint32_t addr)
 {
@@ -101,13 +111,14 @@ __device__ __forceinline__ uint32_t gear_addr(uint32_t laneoff, uint32_t word, i
 // Walker table address of byte k of word: (byte << kWEntShift) | ((lane & 7) << 3).
 __device__ __forceinline__ uint32_t wgear_addr(uint32_t wlaneoff, uint32_t word, int k)
 {
+    if constexpr (kWEntShift == 8) return gear_addr(wlaneoff, word, k);  // 256-B entries: one v_perm
     return (__builtin_amdgcn_ubfe(word, uint32_t(k & 3) * 8u, 8u) << kWEntShift) | wlaneoff;
 }
 
 __device__ __forceinline__ uint32_t key_of(uint64_t fp, uint32_t mlo, uint32_t mhi)
 {
-    // zero iff (fp & mask) == 0
-    return (uint32_t(fp) & mlo) | (uint32_t(fp >> 32) & mhi);
+    // zero iff (fp & mask) == 0: (hi & mhi) | (lo & mlo) in two VALU
+    return __builtin_amdgcn_bitop3_b32(uint32_t(fp >> 32), mhi, uint32_t(fp) & mlo, 0xEA);
 }
 
 __device__ __forceinline__ uint32_t word_of(const uint4 &d, int i)
