@@ -366,7 +366,7 @@ def main():
                 dev_cuts = [c.cpu().numpy().astype(np.uint64) for c in cuts[:len(e2e_cuts)]]
                 same = all(a.shape == d.shape and bool((a == d).all()) for a, d in zip(e2e_cuts, dev_cuts))
                 e2e = dict(value=round(rate, 2), unit="GiB/s", ms_per_call=round(sec * 1e3, 2),
-                           path="cdc_chunk: pageable host -> pinned bounce -> H2D -> kernels -> D2H cut lists",
+                           path="cdc_chunk: pageable host -> H2D (runtime-staged) -> kernels -> D2H cut lists",
                            sample=f"{len(host)} x {host[0].size / GIB:.3g} GiB, {args.e2e_reps} reps",
                            same_cuts_as_device_path=same)
             sample = host

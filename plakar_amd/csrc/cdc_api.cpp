@@ -305,18 +305,28 @@ uint64_t env_mb(const char *name, uint64_t def_mb, uint64_t min_mb)
 
 // Pageable -> pinned copy, split over a few host threads: one thread's
 // memcpy (~10 GB/s) would otherwise cap the PCIe-inclusive rate.
-constexpr int kCopyThreads = 4;
+constexpr int kCopyThreadsMax = 32;
+
+int copy_threads()
+{
+    static const int n = [] {
+        const char *e = getenv("CDC_COPY_THREADS");
+        const int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : (v > kCopyThreadsMax ? kCopyThreadsMax : v);
+    }();
+    return n;
+}
 
 void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t len)
 {
     constexpr uint64_t kMinPiece = 4ull << 20;
-    const int nt = int(std::min<uint64_t>(kCopyThreads, (len + kMinPiece - 1) / kMinPiece));
+    const int nt = int(std::min<uint64_t>(uint64_t(copy_threads()), (len + kMinPiece - 1) / kMinPiece));
     if (nt <= 1) {
         std::memcpy(dst, src, len);
         return;
     }
     const uint64_t per = ((len + nt - 1) / nt + 4095) & ~4095ull;
-    std::thread th[kCopyThreads];
+    std::thread th[kCopyThreadsMax];
     for (int t = 1; t < nt; ++t) {
         const uint64_t o = per * t;
         if (o >= len) break;
@@ -332,6 +342,19 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t len)
 // while the copy engine drains bounce k.
 int stage(DeviceCtx *c, uint8_t *d_dst, const uint8_t *src, uint64_t len)
 {
+    // Direct form (the default; CDC_HOST_DIRECT=0 selects the bounce buffers):
+    // the runtime stages the pageable source itself, 56 GB/s for a pageable
+    // 1-GiB copy on MI355X against ~34 GB/s through these bounce buffers (C4
+    // 32 -> 47 GiB/s end to end).  The call returns when the copy is done; the
+    // previous group's kernels run meanwhile on the compute stream.
+    static const bool direct = [] {
+        const char *e = getenv("CDC_HOST_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    if (direct) {
+        HIPCHK(hipMemcpyAsync(d_dst, src, len, hipMemcpyHostToDevice, c->copy));
+        return CDC_OK;
+    }
     uint64_t off = 0;
     while (off < len) {
         const int k = c->next_bounce;
