@@ -40,7 +40,7 @@ namespace cdc {
 
 static constexpr uint64_t kNoHit = ~0ull;
 #ifndef CDC_RAW_LANE
-#define CDC_RAW_LANE 256
+#define CDC_RAW_LANE 512
 #endif
 static constexpr uint32_t kRawLaneBytes = CDC_RAW_LANE;  // bytes tested per lane per raw-scan block
 static constexpr uint32_t kWarm = 64;           // warm-up bytes (>= W - 1 for any mask)
@@ -109,10 +109,11 @@ __device__ __forceinline__ uint32_t gear_addr(uint32_t laneoff, uint32_t word, i
 }
 
 // Walker table address of byte k of word: (byte << kWEntShift) | ((lane & 7) << 3).
+template <uint32_t ESH = kWEntShift>
 __device__ __forceinline__ uint32_t wgear_addr(uint32_t wlaneoff, uint32_t word, int k)
 {
-    if constexpr (kWEntShift == 8) return gear_addr(wlaneoff, word, k);  // 256-B entries: one v_perm
-    return (__builtin_amdgcn_ubfe(word, uint32_t(k & 3) * 8u, 8u) << kWEntShift) | wlaneoff;
+    if constexpr (ESH == 8) return gear_addr(wlaneoff, word, k);  // 256-B entries: one v_perm
+    return (__builtin_amdgcn_ubfe(word, uint32_t(k & 3) * 8u, 8u) << ESH) | wlaneoff;
 }
 
 __device__ __forceinline__ uint32_t key_of(uint64_t fp, uint32_t mlo, uint32_t mhi)
@@ -126,30 +127,58 @@ __device__ __forceinline__ uint32_t word_of(const uint4 &d, int i)
     return i == 0 ? d.x : i == 1 ? d.y : i == 2 ? d.z : d.w;
 }
 
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // Roll 16 bytes and return the min of the 16 keys (0 iff some position hit).
+// CDC_ROLL_MIN3=1 reduces the keys with v_min3 after the roll instead (C3 5 %
+// slower: the keys stay live across the chain).
+#ifndef CDC_ROLL_MIN3
+#define CDC_ROLL_MIN3 0
+#endif
+template <uint32_t ESH = kWEntShift>
 __device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, const char *tab,
                                                 uint32_t laneoff, uint32_t mlo, uint32_t mhi)
 {
+#if CDC_ROLL_MIN3
+    uint32_t key[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        fp = (fp << 1) + lds_gear(tab, wgear_addr<ESH>(laneoff, word_of(d, k >> 2), k));
+        key[k] = key_of(fp, mlo, mhi);
+    }
+    uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) acc = umin3(acc, key[k], key[k + 1]);
+    return acc;
+#else
     uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        fp = (fp << 1) + lds_gear(tab, wgear_addr(laneoff, word_of(d, k >> 2), k));
+        fp = (fp << 1) + lds_gear(tab, wgear_addr<ESH>(laneoff, word_of(d, k >> 2), k));
         acc = min(acc, key_of(fp, mlo, mhi));
     }
     return acc;
+#endif
 }
 
+template <uint32_t ESH = kWEntShift>
 __device__ __forceinline__ void roll16(const uint4 &d, uint64_t &fp, const char *tab,
                                        uint32_t laneoff)
 {
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-        fp = (fp << 1) + lds_gear(tab, wgear_addr(laneoff, word_of(d, k >> 2), k));
+        fp = (fp << 1) + lds_gear(tab, wgear_addr<ESH>(laneoff, word_of(d, k >> 2), k));
 }
 
 // General 16-byte group at absolute address a: positions < fz have fp = 0
 // (the reference resets fp at p+Min), positions in [ts, te) are tested.
 // Returns the first hit (absolute) or kNoHit; fp is advanced over the group.
+template <uint32_t ESH = kWEntShift>
 __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp, uint64_t a,
                                                     uint64_t ts, uint64_t te, uint64_t fz,
                                                     const char *tab, uint32_t laneoff,
@@ -159,7 +188,7 @@ __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const uint64_t pos = a + k;
-        const uint64_t g = lds_gear(tab, wgear_addr(laneoff, word_of(d, k >> 2), k));
+        const uint64_t g = lds_gear(tab, wgear_addr<ESH>(laneoff, word_of(d, k >> 2), k));
         fp = pos < fz ? 0ull : (fp << 1) + g;
         if (hit == kNoHit && pos >= ts && pos < te && pos >= fz && key_of(fp, mlo, mhi) == 0)
             hit = pos;
@@ -167,12 +196,6 @@ __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp
     return hit;
 }
 
-__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
-{
-    uint32_t r;
-    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
 
 // Copy a uniform value into a VGPR the compiler cannot fold back into an SGPR
 // operand (VOP2 forms with a VGPR mask issue faster than with an SGPR one).
@@ -860,13 +883,24 @@ struct WalkCtx {
     const char *tab;
     uint32_t laneoff;
     uint32_t lane;
+    uint64_t *tab32;        // workgroup's 32-copy table for long raw scans, filled on first use (or null)
+    uint32_t *tab32_ready;  // LDS flag: 1 once tab32 holds the table
+    const uint64_t *gear;   // the 256-entry table in device memory
 };
 
+#ifndef CDC_RAW_TAB32
+#define CDC_RAW_TAB32 0
+#endif
+constexpr uint64_t kTab32MinScan = 32768;  // raw scans at least this long fill and use tab32
+// (CDC_RAW_TAB32=1: C3 +2-4 %, but C1 -4 % from the 80-KiB walker workgroups; off)
+
 // First position in [lo, hi) whose fingerprint (reset to 0 before fz) hits the
-// mask, by a raw scan: lane j rolls its own 256-byte slice of a 16-KiB block
-// after a 64-byte warm-up.  Positions are buffer-relative.
-__device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
-                                  uint32_t mlo, uint32_t mhi)
+// mask, by a raw scan: lane j rolls its own kRawLaneBytes slice of a block
+// after a 64-byte warm-up.  Positions are buffer-relative.  ESH selects the
+// table layout (8: 32 copies, v_perm addresses, conflict-free gathers).
+template <uint32_t ESH>
+__device__ uint64_t raw_scan(const WalkCtx &C, const char *tab, uint32_t laneoff, uint64_t lo, uint64_t hi,
+                             uint64_t fz, uint32_t mlo, uint32_t mhi)
 {
     const uint64_t H = C.ub + hi, FZ = C.ub + fz;
     uint64_t x = C.ub + lo;
@@ -883,15 +917,15 @@ __device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, ui
                 const uint4 d = *reinterpret_cast<const uint4 *>(a);
                 if (a >= FZ && a >= ts && a + 16 <= te) {
                     const uint64_t fp0 = fp;
-                    if (roll16_test(d, fp, C.tab, C.laneoff, mlo, mhi) == 0) {
+                    if (roll16_test<ESH>(d, fp, tab, laneoff, mlo, mhi) == 0) {
                         uint64_t f = fp0;
-                        hit = group_first_hit(d, f, a, ts, te, FZ, C.tab, C.laneoff, mlo, mhi);
+                        hit = group_first_hit<ESH>(d, f, a, ts, te, FZ, tab, laneoff, mlo, mhi);
                         break;
                     }
                 } else if (a >= FZ && a + 16 <= ts) {
-                    roll16(d, fp, C.tab, C.laneoff);
+                    roll16<ESH>(d, fp, tab, laneoff);
                 } else {
-                    hit = group_first_hit(d, fp, a, ts, te, FZ, C.tab, C.laneoff, mlo, mhi);
+                    hit = group_first_hit<ESH>(d, fp, a, ts, te, FZ, tab, laneoff, mlo, mhi);
                     if (hit != kNoHit) break;
                 }
             }
@@ -901,6 +935,26 @@ __device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, ui
         x = bend;
     }
     return kNoHit;
+}
+
+__device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
+                                               uint32_t mlo, uint32_t mhi)
+{
+#if CDC_RAW_TAB32
+    if (C.tab32) {
+        const bool ready = *reinterpret_cast<volatile uint32_t *>(C.tab32_ready) != 0;
+        if (ready || hi - lo >= kTab32MinScan) {
+            if (!ready) {  // this wave fills it; identical concurrent fills by other waves are harmless
+                for (uint32_t i = C.lane; i < 256u * 32u; i += 64u) C.tab32[i] = C.gear[i >> 5];
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (C.lane == 0) *reinterpret_cast<volatile uint32_t *>(C.tab32_ready) = 1u;
+            }
+            return raw_scan<8>(C, reinterpret_cast<const char *>(C.tab32), (C.lane & 31u) << 3, lo, hi, fz, mlo,
+                               mhi);
+        }
+    }
+#endif
+    return raw_scan<kWEntShift>(C, C.tab, C.laneoff, lo, hi, fz, mlo, mhi);
 }
 
 // Truncated window: positions fz + j, j < W - 1, fingerprint started at 0 at
@@ -1226,7 +1280,8 @@ __device__ __forceinline__ uint32_t buf_of_seg(const Batch &B, uint32_t g)
 }
 
 __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, const Workspace &W,
-                                            const char *tab)
+                                            const char *tab, uint64_t *tab32 = nullptr,
+                                            uint32_t *tab32_ready = nullptr)
 {
     WalkCtx C;
     C.ub = reinterpret_cast<uint64_t>(D.data);
@@ -1238,6 +1293,9 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.tab = tab;
     C.lane = threadIdx.x & 63u;
     C.laneoff = (C.lane & (kWCopies - 1u)) << 3;
+    C.tab32 = tab32;
+    C.tab32_ready = tab32_ready;
+    C.gear = W.gear;
     return C;
 }
 
@@ -1249,6 +1307,14 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
 {
     __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
+#if CDC_RAW_TAB32
+    __shared__ uint64_t s_tab32[256 * 32];
+    __shared__ uint32_t s_tab32_ready;
+    if (threadIdx.x == 0) s_tab32_ready = 0u;
+#define CDC_TAB32_ARGS , s_tab32, &s_tab32_ready
+#else
+#define CDC_TAB32_ARGS
+#endif
 #if CDC_WALK_SPEC
     __shared__ uint64_t s_prec[kWalkWavesPerWG][kPreRuns];
     __shared__ SpecBuf s_spec[kWalkWavesPerWG];
@@ -1262,7 +1328,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(co
     if (g >= B.total_segs) return;
     const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab) CDC_TAB32_ARGS);
     const uint64_t q = g - D.seg_base;
     const uint64_t seg_end = (q + 1) * B.seg;
     uint64_t *nodes = W.w1_nodes + size_t(g) * B.cap1;
@@ -1331,6 +1397,14 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk2(co
 {
     __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
+#if CDC_RAW_TAB32
+    __shared__ uint64_t s_tab32[256 * 32];
+    __shared__ uint32_t s_tab32_ready;
+    if (threadIdx.x == 0) s_tab32_ready = 0u;
+#define CDC_TAB32_ARGS , s_tab32, &s_tab32_ready
+#else
+#define CDC_TAB32_ARGS
+#endif
     const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
     const bool l0 = (threadIdx.x & 63u) == 0;
     if (l0) dbg_ts(B, kTsW2 + 8 * g);
@@ -1341,7 +1415,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk2(co
     const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
     if (g == D.seg_base) return;  // segment 0 of a buffer has no junction
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab) CDC_TAB32_ARGS);
     const uint32_t cap1 = B.cap1;
     const uint64_t e = W.w1_exit[g - 1];
     if (l0) dbg_ts(B, kTsW2 + 8 * g + 2, e);
@@ -1425,13 +1499,21 @@ __global__ __launch_bounds__(kSeqThreads) CDC_WALK_ATTR void k_seq(const Batch B
 {
     __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
+#if CDC_RAW_TAB32
+    __shared__ uint64_t s_tab32[256 * 32];
+    __shared__ uint32_t s_tab32_ready;
+    if (threadIdx.x == 0) s_tab32_ready = 0u;
+#define CDC_TAB32_ARGS , s_tab32, &s_tab32_ready
+#else
+#define CDC_TAB32_ARGS
+#endif
     const uint32_t b = blockIdx.x;
     if (!B.force_fallback && W.flags[b] == 0) return;
     fill_gear_lds<kSeqThreads, kWCopies>(s_tab, W.gear);
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const BufDesc &D = B.b[b];
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab));
+    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab) CDC_TAB32_ARGS);
     uint64_t p = 0, idx = 0;
     while (p < C.len) {
         const uint64_t nx = next_node(C, P, p);
