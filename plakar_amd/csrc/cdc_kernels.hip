@@ -873,6 +873,18 @@ __global__ __launch_bounds__(64) void k_selftest_wave(const uint64_t *in, uint32
 // ---------------------------------------------------------------------------
 // Wave-cooperative next(p).
 // ---------------------------------------------------------------------------
+// The walkers' rare paths (raw scans, index runs beyond the first 64) are
+// inlined: as calls they forced 182-198 VGPRs (values kept live in
+// callee-saved registers across the call), inlined the walkers need 125-137.
+#ifndef CDC_WALK_INLINE
+#define CDC_WALK_INLINE 1
+#endif
+#if CDC_WALK_INLINE
+#define CDC_WALK_INL __forceinline__
+#else
+#define CDC_WALK_INL __noinline__
+#endif
+
 struct WalkCtx {
     uint64_t ub;       // absolute address of byte 0
     uint64_t len;
@@ -937,7 +949,7 @@ __device__ uint64_t raw_scan(const WalkCtx &C, const char *tab, uint32_t laneoff
     return kNoHit;
 }
 
-__device__ __noinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
+__device__ CDC_WALK_INL uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
                                                uint32_t mlo, uint32_t mhi)
 {
 #if CDC_RAW_TAB32
@@ -1036,7 +1048,7 @@ __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0
 }
 
 // First full-window MaskS candidate in [a, b) from the run index.
-__device__ __noinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+__device__ CDC_WALK_INL uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
     const uint64_t rl = run_of(C, b - 1);
