@@ -116,6 +116,10 @@ DevParams make_params(const cdc_opts *o)
     const uint64_t ms = g.mask_s << P.fs_sh;
     P.fs_lo = uint32_t(ms);
     P.fs_hi = uint32_t(ms >> 32);
+    P.fl_sh = g.mask_l ? uint32_t(__builtin_clzll(g.mask_l)) : 0u;  // 63 - highest MaskL bit
+    const uint64_t ml = g.mask_l << P.fl_sh;
+    P.fl_lo = uint32_t(ml);
+    P.fl_hi = uint32_t(ml >> 32);
     return P;
 }
 
@@ -216,6 +220,9 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
     W.flags = reinterpret_cast<uint32_t *>(b + pl.off_flags);
     W.w1_exit = reinterpret_cast<uint64_t *>(b + pl.off_w1_exit);
     W.gear = gear;
+    W.runsL = reinterpret_cast<uint64_t *>(b + pl.off_runsL);
+    W.validL = reinterpret_cast<uint32_t *>(b + pl.off_validL);
+    W.sumS = reinterpret_cast<uint32_t *>(b + pl.off_sumS);
     return W;
 }
 
@@ -243,6 +250,12 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         return e ? uint32_t(atoi(e)) : 0u;
     }();
     B.debug = dbg;
+    // CDC_MASKL_INDEX=0 turns the MaskL index off (walkers raw-scan every MaskL region)
+    static const uint32_t mli = [] {
+        const char *e = getenv("CDC_MASKL_INDEX");
+        return e && e[0] == '0' ? 0u : 1u;
+    }();
+    B.maskl_index = mli;
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
     uint32_t segs = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {

@@ -36,6 +36,8 @@ struct DevParams {
     // The scan's shifted frame: fp' = fp << fs_sh (fs_sh = 63 - highest MaskS
     // bit) and MaskS << fs_sh split in 32-bit halves (k_scan).
     uint32_t fs_sh, fs_lo, fs_hi;
+    // The same frame for MaskL (k_scan_l, the MaskL candidate index).
+    uint32_t fl_sh, fl_lo, fl_hi;
 };
 
 struct BufDesc {
@@ -57,6 +59,7 @@ struct Batch {
     uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
     uint32_t scan_lane;      // bytes per scan lane (= per index run); one wave (scan task) = 64 lanes
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
+    uint32_t maskl_index;    // 1: k_scan_l builds the MaskL index of long MaskS-free stretches (walkers use it)
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];
 };
@@ -84,6 +87,12 @@ struct Workspace {
     uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "needs sequential fallback"
     uint64_t *w1_exit;   // [total_segs] last node of the speculative chain (its exit)
     const uint64_t *gear;  // 256 entries, device copy
+    // MaskL candidate index (same record format as runs), built by k_scan_l
+    // only for the scan tasks near a long MaskS-free stretch; validL[task]
+    // says whether task's 64 records are this launch's (1) or absent (0).
+    uint64_t *runsL;     // [total_tasks * 64]
+    uint32_t *validL;    // [total_tasks]
+    uint32_t *sumS;      // [total_tasks] k_scan: MaskS-empty runs of the task (leading | trailing << 8 | longest << 16 | all << 24)
 };
 
 constexpr uint32_t kConvNone = 0xFFFFFFFFu;  // entry was already terminal (chain ended earlier)
@@ -96,7 +105,7 @@ struct Plan {
     uint32_t cap1, cap2;
     uint32_t total_segs, total_tasks;
     size_t off_runs, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_piece, off_flags,
-        off_w1_exit, bytes;
+        off_w1_exit, off_runsL, off_validL, off_sumS, bytes;
 };
 
 // Host-side helpers implemented in cdc_kernels.hip.

@@ -413,19 +413,87 @@ __device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16
     }
 }
 
-__global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
+// Does scan task `t` of buffer D (buffer-relative) need the MaskL index?  The
+// walkers query MaskL candidates at x only after a chunk start p <= x - Normal
+// found no full-window MaskS candidate in [p + Min + W - 1, p + Normal): a
+// MaskS-free stretch of Normal - Min - W + 1 bytes that ends less than
+// Max - Normal before x.  Such a stretch holds at least kc complete runs with
+// no MaskS candidate, so a task is needed only if kc consecutive empty run
+// records occur among the runs from Max - Min before the task to its end.
+// The test only decides where the index is built: a walker that finds no
+// index for a task raw-scans it, so results never depend on it.
+__device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace &W, const BufDesc &D, uint64_t t,
+                             uint32_t lane)
+{
+    const uint64_t sl = B.scan_lane;
+    const uint64_t back = (P.max_size - P.min_size + sl - 1) / sl + 1;   // runs
+    const uint64_t tb = (back + 63) / 64;                                  // tasks
+    const uint64_t t0 = t > tb ? t - tb : 0;
+    const uint64_t gap = P.normal_size - P.min_size - (P.win - 1);
+    const uint32_t kc = uint32_t(gap / sl > 2 ? gap / sl - 1 : 1);
+    const uint32_t *sum = W.sumS + D.task_base;
+    uint32_t cur = 0;
+    for (uint64_t base = t0; base <= t; base += 64) {
+        const uint64_t q = base + lane;
+        const uint32_t v0 = q <= t ? sum[q] : 0u;
+        const uint32_t n = uint32_t(min(t + 1 - base, uint64_t(64)));
+        for (uint32_t l = 0; l < n; ++l) {
+            const uint32_t v = __builtin_amdgcn_readlane(v0, l);
+            const uint32_t lp = v & 0xFFu, ls = (v >> 8) & 0xFFu, li = (v >> 16) & 0xFFu;
+            if (li >= kc) return true;
+            if (v >> 24) {
+                cur += 64;
+            } else {
+                if (cur + lp >= kc) return true;
+                cur = ls;
+            }
+            if (cur >= kc) return true;
+        }
+    }
+    return false;
+}
+
+// MaskS-empty run summary of one scan task (k_scan, for maskl_needed): bit l
+// of `empty` = run l of the task exists and holds no MaskS candidate.
+__device__ __forceinline__ uint32_t empty_summary(uint64_t empty)
+{
+    const uint32_t lead = empty == ~0ull ? 64u : uint32_t(__builtin_ctzll(~empty));
+    const uint32_t trail = empty == ~0ull ? 64u : uint32_t(__builtin_clzll(~empty));
+    uint32_t longest = 0;
+    for (uint64_t m = empty; m; m &= m >> 1) ++longest;
+    return min(lead, 255u) | (min(trail, 255u) << 8) | (min(longest, 255u) << 16) | (empty == ~0ull ? 1u << 24 : 0u);
+}
+
+// The byte scan.  kMaskL = false: the MaskS candidate index of every run
+// (k_scan).  kMaskL = true: the MaskL index (k_scan_l), built only for the
+// tasks maskl_needed() selects; every wave records validL for its task.
+template <bool kMaskL>
+__device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
     __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kNBuf * kStageBytes];
-    if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
-    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, P.fs_sh);
-    __syncthreads();
-    if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
-    const char *tab = s_lds;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
     const uint32_t task = blockIdx.x * kS2Waves + wave;
-    if (task >= B.total_tasks) return;
+    bool act = true;
+    if constexpr (kMaskL) {
+        act = false;
+        if (task < B.total_tasks) {
+            uint32_t bb = 0;
+            while (bb + 1 < B.nbufs && task >= B.b[bb + 1].task_base) ++bb;
+            const BufDesc &Db = B.b[bb];
+            const uint64_t t = task - Db.task_base;
+            if (t * 64ull * B.scan_lane < Db.len) act = maskl_needed(B, P, W, Db, t, lane);
+            if (lane == 0) W.validL[task] = act ? 1u : 0u;
+        }
+        if (!__syncthreads_or(act ? 1 : 0)) return;  // no wave of this workgroup builds the index
+    }
+    if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
+    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, kMaskL ? P.fl_sh : P.fs_sh);
+    __syncthreads();
+    if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
+    const char *tab = s_lds;
+    if (task >= B.total_tasks || !act) return;
     uint32_t b = 0;
     while (b + 1 < B.nbufs && task >= B.b[b + 1].task_base) ++b;
     const BufDesc &D = B.b[b];
@@ -493,8 +561,8 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     };
     const uint32_t TT = T + 1;  // half 1 runs one stage behind
     const int32_t lag = int32_t(kStage * half);
-    const uint32_t vhi = to_vgpr(P.fs_hi);
-    const uint32_t xlo = P.fs_lo, xhi = P.fs_hi;
+    const uint32_t vhi = to_vgpr(kMaskL ? P.fl_hi : P.fs_hi);
+    const uint32_t xlo = kMaskL ? P.fl_lo : P.fs_lo, xhi = kMaskL ? P.fl_hi : P.fs_hi;
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
     using C0 = std::integral_constant<uint32_t, 0>;
     using C1 = std::integral_constant<uint32_t, 1>;
@@ -664,8 +732,8 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
     const uint32_t TT = T;
     const int32_t lag = 0;
 #endif
-    const uint32_t vhi = to_vgpr(P.fs_hi);
-    const uint32_t xlo = P.fs_lo, xhi = P.fs_hi;
+    const uint32_t vhi = to_vgpr(kMaskL ? P.fl_hi : P.fs_hi);
+    const uint32_t xlo = kMaskL ? P.fl_lo : P.fs_lo, xhi = kMaskL ? P.fl_hi : P.fs_hi;
     // buffer-relative position of this lane's first staged byte
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
 
@@ -776,8 +844,22 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
         for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
     }
 #endif
-    if (s < int64_t(D.len)) W.runs[64ull * D.task_base + seg0 + lane] = rec;
-    if (lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
+    if (s < int64_t(D.len)) (kMaskL ? W.runsL : W.runs)[64ull * D.task_base + seg0 + lane] = rec;
+    if constexpr (!kMaskL) {
+        const uint64_t empty = __ballot(s < int64_t(D.len) && (rec & 0xFFFFu) == 0);
+        if (lane == 0) W.sumS[task] = empty_summary(empty);
+    }
+    if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
+}
+
+__global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
+{
+    scan_body<false>(B, P, W);
+}
+
+__global__ __launch_bounds__(kS2Waves * 64) void k_scan_l(const Batch B, const DevParams P, const Workspace W)
+{
+    scan_body<true>(B, P, W);
 }
 
 // DPP helpers (in-row lane shifts, no LDS round trip; ds_bpermute-based
@@ -898,6 +980,8 @@ struct WalkCtx {
     uint64_t *tab32;        // workgroup's 32-copy table for long raw scans, filled on first use (or null)
     uint32_t *tab32_ready;  // LDS flag: 1 once tab32 holds the table
     const uint64_t *gear;   // the 256-entry table in device memory
+    const uint64_t *runsL;  // this buffer's MaskL index records (null: no MaskL index)
+    const uint32_t *validL; // per scan task of the buffer: runsL holds its 64 records
 };
 
 #ifndef CDC_RAW_TAB32
@@ -1026,7 +1110,7 @@ __device__ __forceinline__ uint64_t rec_first(uint64_t rec, uint64_t rs, uint64_
 // `in`): the first candidate in [a, b), rescanning dense runs whose stored
 // entries do not answer.  *done = false when none of these runs holds one.
 __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0, bool in, uint64_t rec, uint64_t a,
-                               uint64_t b, uint64_t fz, bool &done)
+                               uint64_t b, uint64_t fz, bool &done, bool maskl = false)
 {
     const uint64_t rs = (r0 + C.lane) * C.sl;
     const uint64_t cand = in ? rec_first(rec, rs, a, b) : kNoHit;
@@ -1039,7 +1123,7 @@ __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0
         if (lf < ld) return readlane64(cand, lf);
         const uint64_t rr = r0 + uint64_t(ld);
         const uint64_t lo = max(a, rr * C.sl), hi = min(b, (rr + 1) * C.sl);
-        const uint64_t h = raw_first_hit(C, lo, hi, fz, P.ms_lo, P.ms_hi);
+        const uint64_t h = raw_first_hit(C, lo, hi, fz, maskl ? P.ml_lo : P.ms_lo, maskl ? P.ml_hi : P.ms_hi);
         if (h != kNoHit) return h;
         md &= ~(1ull << ld);
     }
@@ -1058,6 +1142,31 @@ __device__ CDC_WALK_INL uint64_t index_first_hit(const WalkCtx &C, const DevPara
         bool done;
         const uint64_t h = recs_first(C, P, r0, in, rec, a, b, fz, done);
         if (done) return h;
+    }
+    return kNoHit;
+}
+
+// First full-window MaskL candidate in [a, b) (a >= the chunk's p + Normal, so
+// every window is full): from the MaskL index for the scan tasks k_scan_l
+// built (64 records per round trip, dense runs rescanned), by a raw scan for
+// the others.
+__device__ CDC_WALK_INL uint64_t maskl_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+                                                 uint64_t fz)
+{
+    if (!C.runsL) return raw_first_hit(C, a, b, fz, P.ml_lo, P.ml_hi);
+    const uint64_t ra = run_of(C, a), rl = run_of(C, b - 1);
+    for (uint64_t r0 = ra & ~63ull; r0 <= rl; r0 += 64) {
+        const uint64_t lo = max(a, r0 * C.sl), hi = min(b, (r0 + 64) * C.sl);
+        if (C.validL[r0 >> 6]) {
+            const bool in = r0 + C.lane >= ra && r0 + C.lane <= rl;
+            const uint64_t rec = in ? C.runsL[r0 + C.lane] : 0ull;
+            bool done;
+            const uint64_t h = recs_first(C, P, r0, in, rec, lo, hi, fz, done, true);
+            if (done) return h;
+        } else {
+            const uint64_t h = raw_first_hit(C, lo, hi, fz, P.ml_lo, P.ml_hi);
+            if (h != kNoHit) return h;
+        }
     }
     return kNoHit;
 }
@@ -1119,10 +1228,10 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
             if (h != kNoHit) return h + P.cut_adj;
         }
     }
-    // ---- MaskL region [p + Normal, p + n): on-demand raw scan
+    // ---- MaskL region [p + Normal, p + n): the MaskL index, or a raw scan
     const uint64_t l_lo = max(norm_end, full0);
     if (l_lo < lim) {
-        h = raw_first_hit(C, l_lo, lim, fz, P.ml_lo, P.ml_hi);
+        h = maskl_first_hit(C, P, l_lo, lim, fz);
         if (h != kNoHit) return h + P.cut_adj;
     }
     return clipped ? kUndet : p + n;
@@ -1308,6 +1417,8 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.tab32 = tab32;
     C.tab32_ready = tab32_ready;
     C.gear = W.gear;
+    C.runsL = B.maskl_index ? W.runsL + 64ull * D.task_base : nullptr;
+    C.validL = B.maskl_index ? W.validL + D.task_base : nullptr;
     return C;
 }
 
@@ -1846,6 +1957,9 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_piece = take(segs * sizeof(Piece));
     plan->off_flags = take(kMaxBufsPerLaunch * 4);
     plan->off_w1_exit = take(segs * 8);
+    plan->off_runsL = take(tasks * 64 * 8);
+    plan->off_validL = take(tasks * 4);
+    plan->off_sumS = take(tasks * 4);
     plan->bytes = off;
     return CDC_OK;
 }
@@ -1909,6 +2023,9 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         }
         return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
     }
+    // MaskL index of the tasks near long MaskS-free stretches (most workgroups
+    // exit after one look at the MaskS index on ordinary data)
+    if (B.total_tasks > 0 && B.maskl_index) hipLaunchKernelGGL(k_scan_l, sgrid, sblock, 0, st, B, P, W);
     if (B.total_segs > 0 && !B.force_fallback) {
         const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
         hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);

@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size-mib", type=int, default=1024)
     ap.add_argument("--workload", default="c1")
+    ap.add_argument("--warm", type=int, default=300, help="launches before the recorded one (clock ramp)")
     args = ap.parse_args()
     os.environ.setdefault("CDC_DEBUG_PHASE", "16")
     import torch
@@ -48,7 +49,7 @@ def main():
     dev = torch.device("cuda", 0)
     bufs = make_buffers(torch, WORKLOADS[args.workload], 0, dev, args.size_mib << 20)
     b = device.DeviceBatch(bufs, chunkers.ChunkerOpts(65536, 1 << 20, 4 << 20))
-    for _ in range(3):
+    for _ in range(max(1, args.warm)):
         b.launch()
     torch.cuda.synchronize()
     ts = np.zeros(K_SLOTS, dtype=np.uint64)
