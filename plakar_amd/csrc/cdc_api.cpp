@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -55,6 +56,11 @@ struct DeviceCtx {
     uint64_t bounce_cap = 0;
     hipEvent_t bounce_ev[kBounces] = {nullptr, nullptr};
     int next_bounce = 0;
+    // Adaptive MaskL index (run_group): k_scan_l raises *hint_h (mapped host
+    // memory) whenever some scan task needed the index; groups launch k_scan_l
+    // while the hint is set, and every 16th group probes when it is not.
+    uint32_t *hint_h = nullptr, *hint_d = nullptr;
+    std::atomic<uint64_t> groups{0};
 };
 
 struct Global {
@@ -250,12 +256,23 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         return e ? uint32_t(atoi(e)) : 0u;
     }();
     B.debug = dbg;
-    // CDC_MASKL_INDEX=0 turns the MaskL index off (walkers raw-scan every MaskL region)
+    // MaskL index (k_scan_l).  CDC_MASKL_INDEX: 0 off (walkers raw-scan every
+    // MaskL region), 1 adaptive (default), 2 every group.  Adaptive: launched
+    // while recent groups on this device needed it (the hint k_scan_l raises),
+    // otherwise on every 16th group as a probe; the hint decays every 1024
+    // groups.  Walkers use the index only in a group that built it, so cut
+    // points never depend on this choice.
     static const uint32_t mli = [] {
         const char *e = getenv("CDC_MASKL_INDEX");
-        return e && e[0] == '0' ? 0u : 1u;
+        return e && (e[0] == '0' || e[0] == '2') ? uint32_t(e[0] - '0') : 1u;
     }();
-    B.maskl_index = mli;
+    {
+        const uint64_t k = ctx->groups.fetch_add(1, std::memory_order_relaxed);
+        volatile uint32_t *hint = ctx->hint_h;
+        if (hint && k % 1024 == 1023) *hint = 0u;
+        B.maskl_index = mli == 2 || (mli == 1 && (k % 16 == 0 || !hint || *hint != 0u)) ? 1u : 0u;
+        B.maskl_hint = ctx->hint_d;
+    }
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
     uint32_t segs = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
@@ -623,6 +640,14 @@ int cdc_init(uint32_t dev_mask, const uint64_t gear[256], uint64_t mask_s, uint6
                 return CDC_E_DEVICE;
             if (hipMalloc(reinterpret_cast<void **>(&c->d_gear), 256 * sizeof(uint64_t)) != hipSuccess)
                 return CDC_E_DEVICE;
+            if (hipHostMalloc(reinterpret_cast<void **>(&c->hint_h), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
+                    hipSuccess) {
+                *c->hint_h = 0u;
+                if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->hint_d), c->hint_h, 0) != hipSuccess) {
+                    (void)hipHostFree(c->hint_h);
+                    c->hint_h = c->hint_d = nullptr;
+                }
+            }
             g.devs.push_back(c);
         }
         if (g.devs.empty()) return CDC_E_NO_DEVICE;
@@ -643,6 +668,8 @@ void cdc_shutdown(void)
     for (auto *c : g.devs) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
+        (void)hipDeviceSynchronize();  // caller streams may still run kernels that write the hint
+        if (c->hint_h) (void)hipHostFree(c->hint_h);
         if (c->d_gear) (void)hipFree(c->d_gear);
         if (c->copy) (void)hipStreamSynchronize(c->copy);
         free_ctx_buffers(c);

@@ -60,6 +60,7 @@ struct Batch {
     uint32_t scan_lane;      // bytes per scan lane (= per index run); one wave (scan task) = 64 lanes
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
     uint32_t maskl_index;    // 1: k_scan_l builds the MaskL index of long MaskS-free stretches (walkers use it)
+    uint32_t *maskl_hint;    // mapped host word: k_scan_l sets it when some task needed the MaskL index
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];
 };

@@ -487,6 +487,8 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             if (lane == 0) W.validL[task] = act ? 1u : 0u;
         }
         if (!__syncthreads_or(act ? 1 : 0)) return;  // no wave of this workgroup builds the index
+        if (threadIdx.x == 0 && B.maskl_hint)
+            __hip_atomic_store(B.maskl_hint, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, kMaskL ? P.fl_sh : P.fs_sh);
