@@ -9,7 +9,8 @@ ksub = sys.argv[2] if len(sys.argv) > 2 else "k_scan"
 agg = collections.defaultdict(list)
 for p in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv") + glob.glob(f"{d}/run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
-        if ksub in r["Kernel_Name"]:
+        name = r["Kernel_Name"].split("(")[0].split(" ")[-1]
+        if name == ksub or name.endswith("::" + ksub):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg.items()):
     print(f"{k:28s} n={len(v):3d} avg={sum(v)/len(v):.5g}")
