@@ -178,7 +178,7 @@ def digest_leg(torch, batch, bufs, reps, check):
     return d
 
 
-def cpu_baseline(bufs_host, cuts_dev, opts, seconds):
+def cpu_baseline(bufs_host, cuts_dev, opts, seconds, threads=1):
     """The CPU oracle (scalar C restatement of the reference chunker, 1 thread)
     timed on a bounded sample of the same workload; also checks that the GPU
     cut lists of that sample are bit-identical."""
@@ -204,10 +204,32 @@ def cpu_baseline(bufs_host, cuts_dev, opts, seconds):
         el = time.perf_counter() - t0
         if el >= seconds or reps >= 1024:  # the time bound governs
             break
-    return dict(value=done_bytes / el / GIB, unit="GiB/s", cores=1, kind="port",
-                sample=f"{len(bufs_host)} buffer(s) x {bufs_host[0].size / GIB:.3g} GiB, {reps} rep(s), "
-                       f"{el:.1f} s, scalar C oracle (oracle/fastcdc_oracle.c), 1 thread, host of the GPU box "
-                       f"(nproc={os.cpu_count()})"), parity
+    one = dict(value=done_bytes / el / GIB, unit="GiB/s", cores=1, kind="port",
+               sample=f"{len(bufs_host)} buffer(s) x {bufs_host[0].size / GIB:.3g} GiB, {reps} rep(s), "
+                      f"{el:.1f} s, scalar C oracle (oracle/fastcdc_oracle.c), 1 thread, host of the GPU box "
+                      f"(nproc={os.cpu_count()})")
+    if threads > 1:
+        one["multi_thread"] = cpu_threads_leg(orc, gear, kw, bufs_host, threads, seconds / 2)
+    return one, parity
+
+
+def cpu_threads_leg(orc, gear, kw, bufs_host, threads, seconds):
+    """the same oracle on N host threads, one independent
+    64-MiB piece of the sample per call (plakar chunks files concurrently, one
+    goroutine per file). ctypes drops the GIL for the C call."""
+    from concurrent.futures import ThreadPoolExecutor
+    piece = 64 << 20
+    parts = [a[o:o + piece] for a in bufs_host for o in range(0, a.size, piece)]
+    done_bytes, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while True:
+            done_bytes += sum(ex.map(lambda x: (orc.chunk(x, gear, **kw), x.size)[1], parts))
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    return dict(value=round(done_bytes / el / GIB, 2), unit="GiB/s", cores=threads, kind="port",
+                sample=f"{len(parts)} independent 64-MiB pieces of the sample per round, {done_bytes / GIB:.0f} GiB "
+                       f"in {el:.1f} s, {threads} threads")
 
 
 def main():
@@ -221,6 +243,8 @@ def main():
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
     ap.add_argument("--size-mib", type=int, default=0, help="override the per-buffer size (debug)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="threads of the multi-threaded CPU oracle leg (16 = the GPU box's CPU share; 1 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="device workloads: consecutive steps alternate over this many streams, each with its "
@@ -372,7 +396,7 @@ def main():
             sample = host
             sample_cuts = cuts[:1]
         if not args.no_cpu_baseline:
-            baseline, parity = cpu_baseline(sample, sample_cuts, opts, args.cpu_seconds)
+            baseline, parity = cpu_baseline(sample, sample_cuts, opts, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         config = {"workload": wl["desc"], "bytes_per_gpu": per_rank_bytes,
