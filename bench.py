@@ -57,7 +57,8 @@ def reduce_max(dist, world, value, dev):
     if world == 1:
         return value
     import torch
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=dev if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -271,11 +272,20 @@ def main():
 
     from plakar_amd import _lib, chunkers, device
 
+    # BENCH_REHEARSE_ONE_GPU=1: every rank on device 0 over gloo, to rehearse
+    # the N-rank launch, barrier and max-over-ranks timing on a one-GPU box.
+    # The numbers of such a run are not a scaling measurement.
+    rehearse = os.environ.get("BENCH_REHEARSE_ONE_GPU") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     def barrier():
         if world > 1:
