@@ -206,6 +206,15 @@ void cdc_chunker_free(cdc_chunker *c);
  * on the device, for cross-checking the fast path). */
 int cdc_set_debug_mode(int mode);
 
+/* When the MaskL candidate index (k_scan_l) is built: 0 = never (walkers
+ * raw-scan every MaskL region), 1 = adaptive (default: while recent launch
+ * groups on the device needed it, and every 16th group as a probe), 2 = every
+ * launch group.  Cut points never depend on it; tests use it to cover every
+ * path.  Initial value from the CDC_MASKL_INDEX environment variable.  Not a
+ * reference interface (the Go chunker has no index).  Returns CDC_OK or
+ * CDC_E_INVALID. */
+int cdc_set_maskl_index_mode(int mode);
+
 /* Live profiling of the device path: when enabled, every launch group records
  * hipEvents on its stream before/after the scan kernel and after the last
  * resolution kernel.  collect() waits for the recorded events, returns the

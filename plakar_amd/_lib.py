@@ -101,6 +101,7 @@ SIGNATURES = {
                                                             _P(ctypes.c_void_p), _P(ctypes.c_void_p),
                                                             _P(ctypes.c_void_p), ctypes.c_void_p]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),
                                            _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),

@@ -79,6 +79,16 @@ Global &G()
     return g;
 }
 
+// MaskL index mode (cdc_set_maskl_index_mode; initial value from CDC_MASKL_INDEX)
+std::atomic<uint32_t> &maskl_index_mode()
+{
+    static std::atomic<uint32_t> m([] {
+        const char *e = getenv("CDC_MASKL_INDEX");
+        return e && (e[0] == '0' || e[0] == '2') ? uint32_t(e[0] - '0') : 1u;
+    }());
+    return m;
+}
+
 uint64_t splitmix64(uint64_t &s)
 {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -262,10 +272,7 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     // otherwise on every 16th group as a probe; the hint decays every 1024
     // groups.  Walkers use the index only in a group that built it, so cut
     // points never depend on this choice.
-    static const uint32_t mli = [] {
-        const char *e = getenv("CDC_MASKL_INDEX");
-        return e && (e[0] == '0' || e[0] == '2') ? uint32_t(e[0] - '0') : 1u;
-    }();
+    const uint32_t mli = maskl_index_mode().load(std::memory_order_relaxed);
     {
         const uint64_t k = ctx->groups.fetch_add(1, std::memory_order_relaxed);
         volatile uint32_t *hint = ctx->hint_h;
@@ -602,6 +609,13 @@ int cdc_validate(const char *algorithm, const cdc_opts *opts)
 int cdc_set_debug_mode(int mode)
 {
     G().debug_mode = mode;
+    return CDC_OK;
+}
+
+int cdc_set_maskl_index_mode(int mode)
+{
+    if (mode < 0 || mode > 2) return CDC_E_INVALID;
+    maskl_index_mode().store(uint32_t(mode), std::memory_order_relaxed);
     return CDC_OK;
 }
 

@@ -86,3 +86,9 @@ def chunk_device(tensors, opts, final=True):
 def set_debug_mode(mode):
     """0 = fast path, 1 = sequential single-wave resolver (cross-check)."""
     lib().cdc_set_debug_mode(int(mode))
+
+
+def set_maskl_index_mode(mode):
+    """0 = never build the MaskL index, 1 = adaptive (default), 2 = every
+    launch group. Cut points do not depend on it."""
+    check(lib().cdc_set_maskl_index_mode(int(mode)))

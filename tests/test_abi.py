@@ -40,6 +40,15 @@ def test_abi_version_and_defaults():
     assert (o.min_size, o.normal_size, o.max_size) == (65536, 1 << 20, 4 << 20)
 
 
+def test_maskl_index_mode_setter():
+    """Device-free knob: valid modes 0-2, anything else CDC_E_INVALID."""
+    L = _lib.lib()
+    assert L.cdc_set_maskl_index_mode(3) == _lib.CDC_E_INVALID
+    assert L.cdc_set_maskl_index_mode(-1) == _lib.CDC_E_INVALID
+    for m in (0, 2, 1):
+        assert L.cdc_set_maskl_index_mode(m) == 0
+
+
 def test_default_gear_is_the_committed_placeholder():
     with open(os.path.join(ROOT, "tests", "golden", "gear_placeholder.json")) as f:
         fx = [int(x, 16) for x in json.load(f)["gear"]]

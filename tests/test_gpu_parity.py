@@ -60,6 +60,7 @@ def _reset_debug():
     device.set_debug_mode(0)
     yield
     device.set_debug_mode(0)
+    device.set_maskl_index_mode(1)
     _lib.ensure_init(gear=_lib.default_gear())
 
 
@@ -151,6 +152,23 @@ def test_device_alternative_masks(oracle):
     (c,), _ = b.results()
     got = c.cpu().numpy().astype(np.uint64)
     assert_same(got, oracle.chunk(data, gear_table(50), mask_s=ms, mask_l=ml, **p), "masks")
+
+
+# ---------------------------------------------------------------- MaskL index modes
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_maskl_index_modes(oracle, mode):
+    """C3-like data (zeros + 1 % random bytes): a quarter of the chunks pass
+    Normal and end on MaskL candidates. Never / adaptive / always building the
+    MaskL index (k_scan_l) gives the same cuts; several launches so adaptive
+    mode runs both with and without the index."""
+    data = low_entropy(48 << 20, 71)
+    gear = _placeholder()
+    ref = oracle.chunk(data, gear, **DEF)
+    assert (ref[:, 1] > DEF["normal_size"]).any(), "no chunk reaches the MaskL region"
+    device.set_maskl_index_mode(mode)
+    for rep in range(3):
+        (got,), _ = gpu_chunk([data], DEF, gear=gear)
+        assert_same(got, ref, f"maskl mode {mode} rep {rep}")
 
 
 # ---------------------------------------------------------------- debug resolver
