@@ -238,7 +238,6 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
     W.gear = gear;
     W.runsL = reinterpret_cast<uint64_t *>(b + pl.off_runsL);
     W.validL = reinterpret_cast<uint32_t *>(b + pl.off_validL);
-    W.sumS = reinterpret_cast<uint32_t *>(b + pl.off_sumS);
     return W;
 }
 

@@ -93,7 +93,6 @@ struct Workspace {
     // says whether task's 64 records are this launch's (1) or absent (0).
     uint64_t *runsL;     // [total_tasks * 64]
     uint32_t *validL;    // [total_tasks]
-    uint32_t *sumS;      // [total_tasks] k_scan: MaskS-empty runs of the task (leading | trailing << 8 | longest << 16 | all << 24)
 };
 
 constexpr uint32_t kConvNone = 0xFFFFFFFFu;  // entry was already terminal (chain ended earlier)
@@ -106,7 +105,7 @@ struct Plan {
     uint32_t cap1, cap2;
     uint32_t total_segs, total_tasks;
     size_t off_runs, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_piece, off_flags,
-        off_w1_exit, off_runsL, off_validL, off_sumS, bytes;
+        off_w1_exit, off_runsL, off_validL, bytes;
 };
 
 // Host-side helpers implemented in cdc_kernels.hip.

@@ -413,55 +413,72 @@ __device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16
     }
 }
 
-// Does scan task `t` of buffer D (buffer-relative) need the MaskL index?  The
-// walkers query MaskL candidates at x only after a chunk start p <= x - Normal
-// found no full-window MaskS candidate in [p + Min + W - 1, p + Normal): a
-// MaskS-free stretch of Normal - Min - W + 1 bytes that ends less than
-// Max - Normal before x.  Such a stretch holds at least kc complete runs with
-// no MaskS candidate, so a task is needed only if kc consecutive empty run
-// records occur among the runs from Max - Min before the task to its end.
-// The test only decides where the index is built: a walker that finds no
-// index for a task raw-scans it, so results never depend on it.
+// Does scan task `t` of buffer D (buffer-relative) need the MaskL index?  A
+// walker queries MaskL candidates from x0 = p + Normal only when the chunk start p found no full-window MaskS
+// candidate in [p + Min + W - 1, p + Normal): a MaskS-free interval of
+// Normal - Min - W + 1 bytes, holding at least kc complete MaskS index runs
+// with no candidate.  In MaskS-run units, with [a, b) the maximal empty
+// stretch holding those runs, x0 lies in runs a + kc .. b (run b, the first
+// non-empty one, may hold x0 before its first candidate), and the search then
+// runs to the first MaskL candidate past x0.  So a run r needs the index if
+// r >= a + kc - 1 inside such a stretch, or if r <= b + kMaskLSpill after
+// one; a longer search past the spill raw-scans.  The test reads the MaskS
+// run records from kc + spill runs before the task to its end (256 per round
+// trip, one ballot per 64) and steps over the non-empty runs of each word.
+// It only decides where the index is built: a walker that
+// finds no index for a task raw-scans it, so results never depend on it.
+#ifndef CDC_MASKL_SPILL
+#define CDC_MASKL_SPILL 16
+#endif
+constexpr uint64_t kMaskLSpill = CDC_MASKL_SPILL;  // MaskS runs after a long stretch's end
+
 __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace &W, const BufDesc &D, uint64_t t,
                              uint32_t lane)
 {
-    const uint64_t sl = B.scan_lane;
-    const uint64_t back = (P.max_size - P.min_size + sl - 1) / sl + 1;   // runs
-    const uint64_t tb = (back + 63) / 64;                                  // tasks
-    const uint64_t t0 = t > tb ? t - tb : 0;
+    const uint64_t sl = B.scan_lane, tb = 64ull * sl;
+    const uint64_t start = t * tb, end = min(D.len, start + tb);
+    const uint64_t ra = start / sl, rb = (end - 1) / sl;  // the task's runs
     const uint64_t gap = P.normal_size - P.min_size - (P.win - 1);
     const uint32_t kc = uint32_t(gap / sl > 2 ? gap / sl - 1 : 1);
-    const uint32_t *sum = W.sumS + D.task_base;
-    uint32_t cur = 0;
-    for (uint64_t base = t0; base <= t; base += 64) {
-        const uint64_t q = base + lane;
-        const uint32_t v0 = q <= t ? sum[q] : 0u;
-        const uint32_t n = uint32_t(min(t + 1 - base, uint64_t(64)));
-        for (uint32_t l = 0; l < n; ++l) {
-            const uint32_t v = __builtin_amdgcn_readlane(v0, l);
-            const uint32_t lp = v & 0xFFu, ls = (v >> 8) & 0xFFu, li = (v >> 16) & 0xFFu;
-            if (li >= kc) return true;
-            if (v >> 24) {
-                cur += 64;
-            } else {
-                if (cur + lp >= kc) return true;
-                cur = ls;
+    const uint64_t r_lo = ra > kc + kMaskLSpill ? ra - kc - kMaskLSpill : 0;
+    const uint64_t *runs = W.runs + 64ull * D.task_base;
+    uint32_t cur = 0;               // empty runs ending at the current one
+    uint64_t last_end = ~0ull;      // b of the latest long stretch (~0: none)
+    for (uint64_t r4 = r_lo; r4 <= rb; r4 += 256) {
+        uint64_t rec[4];  // four words of records in flight: one round trip per 256 runs
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t q = r4 + 64u * j + lane;
+            rec[j] = q <= rb ? runs[q] : 1ull;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t r0 = r4 + 64u * j;
+            if (r0 > rb) break;
+            const uint64_t E = __ballot((rec[j] & 0xFFFFu) == 0);
+            const uint32_t n = uint32_t(min(rb + 1 - r0, uint64_t(64)));
+            // walk the word's non-empty runs (Z); the empty runs between them
+            // extend the current stretch
+            uint64_t Z = ~E & (n == 64 ? ~0ull : (1ull << n) - 1);
+            uint32_t pos = 0;
+            while (true) {
+                const uint32_t z = Z ? uint32_t(__builtin_ctzll(Z)) : n;  // next non-empty run (or the end)
+                if (z > pos) {  // runs r0 + pos .. r0 + z - 1 empty: run r0 + pos + i ends a stretch of cur + i + 1
+                    const uint64_t first = r0 + pos + (cur + 1 >= kc ? 0u : kc - cur - 1);
+                    if (max(first, ra) <= r0 + z - 1) return true;
+                    cur += z - pos;
+                }
+                if (z >= n) break;
+                const uint64_t r = r0 + z;
+                if (cur >= kc) last_end = r;
+                cur = 0;
+                if (r >= ra && last_end != ~0ull && r - last_end <= kMaskLSpill) return true;
+                Z &= Z - 1;
+                pos = z + 1;
             }
-            if (cur >= kc) return true;
         }
     }
     return false;
-}
-
-// MaskS-empty run summary of one scan task (k_scan, for maskl_needed): bit l
-// of `empty` = run l of the task exists and holds no MaskS candidate.
-__device__ __forceinline__ uint32_t empty_summary(uint64_t empty)
-{
-    const uint32_t lead = empty == ~0ull ? 64u : uint32_t(__builtin_ctzll(~empty));
-    const uint32_t trail = empty == ~0ull ? 64u : uint32_t(__builtin_clzll(~empty));
-    uint32_t longest = 0;
-    for (uint64_t m = empty; m; m &= m >> 1) ++longest;
-    return min(lead, 255u) | (min(trail, 255u) << 8) | (min(longest, 255u) << 16) | (empty == ~0ull ? 1u << 24 : 0u);
 }
 
 // The byte scan.  kMaskL = false: the MaskS candidate index of every run
@@ -847,10 +864,6 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     }
 #endif
     if (s < int64_t(D.len)) (kMaskL ? W.runsL : W.runs)[64ull * D.task_base + seg0 + lane] = rec;
-    if constexpr (!kMaskL) {
-        const uint64_t empty = __ballot(s < int64_t(D.len) && (rec & 0xFFFFu) == 0);
-        if (lane == 0) W.sumS[task] = empty_summary(empty);
-    }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
 
@@ -1961,7 +1974,6 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_w1_exit = take(segs * 8);
     plan->off_runsL = take(tasks * 64 * 8);
     plan->off_validL = take(tasks * 4);
-    plan->off_sumS = take(tasks * 4);
     plan->bytes = off;
     return CDC_OK;
 }
