@@ -424,7 +424,7 @@ __device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16
 // r >= a + kc - 1 inside such a stretch, or if r <= b + kMaskLSpill after
 // one; a longer search past the spill raw-scans.  The test reads the MaskS
 // run records from kc + spill runs before the task to its end (256 per round
-// trip, one ballot per 64) and steps over the non-empty runs of each word.
+// trip) and decides each 64-run word with one lane per run and one ballot.
 // It only decides where the index is built: a walker that
 // finds no index for a task raw-scans it, so results never depend on it.
 #ifndef CDC_MASKL_SPILL
@@ -435,6 +435,9 @@ constexpr uint64_t kMaskLSpill = CDC_MASKL_SPILL;  // MaskS runs after a long st
 __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace &W, const BufDesc &D, uint64_t t,
                              uint32_t lane)
 {
+#if CDC_DIAG_MASKL_TEST == 1
+    return false;
+#endif
     const uint64_t sl = B.scan_lane, tb = 64ull * sl;
     const uint64_t start = t * tb, end = min(D.len, start + tb);
     const uint64_t ra = start / sl, rb = (end - 1) / sl;  // the task's runs
@@ -442,8 +445,7 @@ __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace
     const uint32_t kc = uint32_t(gap / sl > 2 ? gap / sl - 1 : 1);
     const uint64_t r_lo = ra > kc + kMaskLSpill ? ra - kc - kMaskLSpill : 0;
     const uint64_t *runs = W.runs + 64ull * D.task_base;
-    uint32_t cur = 0;               // empty runs ending at the current one
-    uint64_t last_end = ~0ull;      // b of the latest long stretch (~0: none)
+    uint32_t cur = 0;  // empty runs ending just before the current word
     for (uint64_t r4 = r_lo; r4 <= rb; r4 += 256) {
         uint64_t rec[4];  // four words of records in flight: one round trip per 256 runs
 #pragma unroll
@@ -457,25 +459,29 @@ __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace
             if (r0 > rb) break;
             const uint64_t E = __ballot((rec[j] & 0xFFFFu) == 0);
             const uint32_t n = uint32_t(min(rb + 1 - r0, uint64_t(64)));
-            // walk the word's non-empty runs (Z); the empty runs between them
-            // extend the current stretch
-            uint64_t Z = ~E & (n == 64 ? ~0ull : (1ull << n) - 1);
-            uint32_t pos = 0;
-            while (true) {
-                const uint32_t z = Z ? uint32_t(__builtin_ctzll(Z)) : n;  // next non-empty run (or the end)
-                if (z > pos) {  // runs r0 + pos .. r0 + z - 1 empty: run r0 + pos + i ends a stretch of cur + i + 1
-                    const uint64_t first = r0 + pos + (cur + 1 >= kc ? 0u : kc - cur - 1);
-                    if (max(first, ra) <= r0 + z - 1) return true;
-                    cur += z - pos;
-                }
-                if (z >= n) break;
-                const uint64_t r = r0 + z;
-                if (cur >= kc) last_end = r;
-                cur = 0;
-                if (r >= ra && last_end != ~0ull && r - last_end <= kMaskLSpill) return true;
-                Z &= Z - 1;
-                pos = z + 1;
+#if CDC_DIAG_MASKL_TEST == 2
+            if (E == 0x123456789ull + n) return true;
+            continue;
+#endif
+            // Lane i looks at run r = r0 + i: the empty stretch ending at
+            // r - 1 has `prev` runs (from the word's non-empty runs Z below
+            // i, or cur + i when there are none).  An empty run needs the
+            // index once its stretch reaches kc; a non-empty run after a long
+            // stretch is that stretch's end b, which makes [b, b + spill]
+            // need it.
+            const uint64_t Z = ~E & (n == 64 ? ~0ull : (1ull << n) - 1);
+            const uint64_t below = Z & ((1ull << lane) - 1);
+            const uint32_t prev = below ? lane - 1u - (63u - uint32_t(__builtin_clzll(below))) : cur + lane;
+            const uint64_t r = r0 + lane;
+            bool need = false;
+            if (lane < n) {
+                if ((E >> lane) & 1ull)
+                    need = r >= ra && prev + 1 >= kc;
+                else
+                    need = prev >= kc && r + kMaskLSpill >= ra;  // r <= rb holds
             }
+            if (__ballot(need)) return true;
+            cur = Z ? n - 1u - (63u - uint32_t(__builtin_clzll(Z))) : cur + n;
         }
     }
     return false;

@@ -3,7 +3,7 @@
 # previous build (plakar_amd/_lib/variants/old.so, built beforehand from the
 # earlier sources) against the current one on C3 and C1.
 set -e
-OUT=gpurun_out/mlsel; mkdir -p $OUT
+OUT=gpurun_out/mlsel4; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 tail -1 $OUT/gpu_tests.log
