@@ -282,7 +282,7 @@ constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane pe
 constexpr uint32_t kGroups = kStage / 16;             // 16-byte groups per stage
 static_assert(kStage == 32 || kStage == 64 || kStage == 128, "stage size");
 constexpr uint32_t kNBuf = CDC_SCAN_NBUF;             // ring depth (kNBuf - 1 stages in flight)
-constexpr uint32_t kAhead = kNBuf - 1;
+[[maybe_unused]] constexpr uint32_t kAhead = kNBuf - 1;
 constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
 static_assert(kNBuf >= 1 && kNBuf <= 3, "ring depth");
@@ -1008,7 +1008,7 @@ struct WalkCtx {
 #ifndef CDC_RAW_TAB32
 #define CDC_RAW_TAB32 0
 #endif
-constexpr uint64_t kTab32MinScan = 32768;  // raw scans at least this long fill and use tab32
+[[maybe_unused]] constexpr uint64_t kTab32MinScan = 32768;  // raw scans at least this long fill and use tab32
 // (CDC_RAW_TAB32=1: C3 +2-4 %, but C1 -4 % from the 80-KiB walker workgroups; off)
 
 // First position in [lo, hi) whose fingerprint (reset to 0 before fz) hits the
