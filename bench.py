@@ -373,7 +373,7 @@ def main():
     achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
     roofline = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=load_traffic(args.workload),
-                    kernel="k_scan", kernel_avg_ms=round(scan_avg_ms, 4),
+                    kernel="k_scan (k_scan_f while the MaskL index is fused into it)", kernel_avg_ms=round(scan_avg_ms, 4),
                     algorithmic_bytes_per_launch=int(bytes_per_launch),
                     timed_passes=n,
                     pipeline_avg_ms=round(pipe_avg_ms, 4))

@@ -206,10 +206,11 @@ void cdc_chunker_free(cdc_chunker *c);
  * on the device, for cross-checking the fast path). */
 int cdc_set_debug_mode(int mode);
 
-/* When the MaskL candidate index (k_scan_l) is built: 0 = never (walkers
+/* When and how the MaskL candidate index is built: 0 = never (walkers
  * raw-scan every MaskL region), 1 = adaptive (default: while recent launch
- * groups on the device needed it, and every 16th group as a probe), 2 = every
- * launch group.  Cut points never depend on it; tests use it to cover every
+ * groups on the device needed it, in the same pass as the MaskS index
+ * (k_scan_f), and on every 16th group as a probe by k_scan_l), 2 = every
+ * launch group in the fused pass, 3 = every launch group by k_scan_l.  Cut points never depend on it; tests use it to cover every
  * path.  Initial value from the CDC_MASKL_INDEX environment variable.  Not a
  * reference interface (the Go chunker has no index).  Returns CDC_OK or
  * CDC_E_INVALID. */

@@ -84,7 +84,7 @@ std::atomic<uint32_t> &maskl_index_mode()
 {
     static std::atomic<uint32_t> m([] {
         const char *e = getenv("CDC_MASKL_INDEX");
-        return e && (e[0] == '0' || e[0] == '2') ? uint32_t(e[0] - '0') : 1u;
+        return e && (e[0] == '0' || e[0] == '2' || e[0] == '3') ? uint32_t(e[0] - '0') : 1u;
     }());
     return m;
 }
@@ -133,6 +133,17 @@ DevParams make_params(const cdc_opts *o)
     P.fs_lo = uint32_t(ms);
     P.fs_hi = uint32_t(ms >> 32);
     P.fl_sh = g.mask_l ? uint32_t(__builtin_clzll(g.mask_l)) : 0u;  // 63 - highest MaskL bit
+    P.fm_ws = P.fm_m = P.fm_ok = 0u;
+    if (g.mask_l && __builtin_clzll(g.mask_l) >= int(P.fs_sh)) {  // MaskL << fs_sh keeps every bit
+        const uint64_t lf = g.mask_l << P.fs_sh;
+        const uint32_t hb = 63u - uint32_t(__builtin_clzll(lf)), lb = uint32_t(__builtin_ctzll(lf));
+        const uint32_t ws = hb >= 31u ? hb - 31u : 0u;
+        if (lb >= ws && ws <= 31u) {
+            P.fm_ws = ws;
+            P.fm_m = uint32_t(lf >> ws);
+            P.fm_ok = 1u;
+        }
+    }
     const uint64_t ml = g.mask_l << P.fl_sh;
     P.fl_lo = uint32_t(ml);
     P.fl_hi = uint32_t(ml >> 32);
@@ -276,7 +287,11 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         const uint64_t k = ctx->groups.fetch_add(1, std::memory_order_relaxed);
         volatile uint32_t *hint = ctx->hint_h;
         if (hint && k % 1024 == 1023) *hint = 0u;
-        B.maskl_index = mli == 2 || (mli == 1 && (k % 16 == 0 || !hint || *hint != 0u)) ? 1u : 0u;
+        const bool hinted = !hint || *hint != 0u;
+        B.maskl_index = mli >= 2 || (mli == 1 && (k % 16 == 0 || hinted)) ? 1u : 0u;
+        // fused (k_scan_f: both indexes in one pass over the bytes) while the
+        // hint says the index is needed; the probes re-check with k_scan_l
+        B.maskl_fused = P.fm_ok && (mli == 2 || (mli == 1 && hinted)) ? 1u : 0u;
         B.maskl_hint = ctx->hint_d;
     }
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
@@ -613,7 +628,7 @@ int cdc_set_debug_mode(int mode)
 
 int cdc_set_maskl_index_mode(int mode)
 {
-    if (mode < 0 || mode > 2) return CDC_E_INVALID;
+    if (mode < 0 || mode > 3) return CDC_E_INVALID;
     maskl_index_mode().store(uint32_t(mode), std::memory_order_relaxed);
     return CDC_OK;
 }

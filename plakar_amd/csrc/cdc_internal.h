@@ -38,6 +38,10 @@ struct DevParams {
     uint32_t fs_sh, fs_lo, fs_hi;
     // The same frame for MaskL (k_scan_l, the MaskL candidate index).
     uint32_t fl_sh, fl_lo, fl_hi;
+    // MaskL inside the MaskS frame (k_scan_f): the 32-bit window of fp' from
+    // bit fm_ws holds every bit of MaskL << fs_sh; its mask fm_m.  fm_ok = 0
+    // when no such window exists (then k_scan + k_scan_l only).
+    uint32_t fm_ws, fm_m, fm_ok;
 };
 
 struct BufDesc {
@@ -60,6 +64,7 @@ struct Batch {
     uint32_t scan_lane;      // bytes per scan lane (= per index run); one wave (scan task) = 64 lanes
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
     uint32_t maskl_index;    // 1: k_scan_l builds the MaskL index of long MaskS-free stretches (walkers use it)
+    uint32_t maskl_fused;    // 1 (with maskl_index): k_scan_f builds both indexes of every task in one pass
     uint32_t *maskl_hint;    // mapped host word: k_scan_l sets it when some task needed the MaskL index
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];

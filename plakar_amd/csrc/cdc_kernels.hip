@@ -487,12 +487,29 @@ __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace
     return false;
 }
 
+// Exact MaskL test of one 16-byte group inside the MaskS frame (k_scan_f):
+// the window of fp' from bit ws holds all of MaskL's bits, so the fused
+// filter is exact and this only records the positions.
+__device__ __forceinline__ void record_l_group(uint64_t f, const uint64_t (&g)[16], int32_t r0, int32_t len,
+                                               uint32_t ws, uint32_t m, uint64_t &rec)
+{
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        f = (f << 1) + g[k];
+        const int32_t r = r0 + k;
+        if ((__builtin_amdgcn_alignbit(uint32_t(f >> 32), uint32_t(f), ws) & m) == 0 && r >= 0 && r < len)
+            record_hit(rec, r);
+    }
+}
+
 // The byte scan.  kMaskL = false: the MaskS candidate index of every run
 // (k_scan).  kMaskL = true: the MaskL index (k_scan_l), built only for the
 // tasks maskl_needed() selects; every wave records validL for its task.
-template <bool kMaskL>
+template <bool kMaskL, bool kFused = false>
 __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
+    static_assert(!(kMaskL && kFused), "k_scan_f builds both indexes in the MaskS frame");
+    static_assert(!kFused || CDC_SCAN_V2, "k_scan_f needs the v2 staging");
     __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kNBuf * kStageBytes];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -587,6 +604,7 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     const uint32_t TT = T + 1;  // half 1 runs one stage behind
     const int32_t lag = int32_t(kStage * half);
     const uint32_t vhi = to_vgpr(kMaskL ? P.fl_hi : P.fs_hi);
+    const uint32_t vlm = kFused ? to_vgpr(P.fm_m) : 0u, lws = P.fm_ws;  // k_scan_f: MaskL window
     const uint32_t xlo = kMaskL ? P.fl_lo : P.fs_lo, xhi = kMaskL ? P.fl_hi : P.fs_hi;
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
     using C0 = std::integral_constant<uint32_t, 0>;
@@ -613,6 +631,7 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(Bv[0], k >> 2), k));
     uint64_t fp = 0;
     uint64_t rec = 0;
+    uint64_t recL = 0;  // k_scan_f: the run's MaskL record
     const int32_t len = int32_t(e - s);
     const int32_t rr0 = int32_t(rel0 - s) - lag;
     // One stage t of parity Q: rolls cur (stage t's data); at its last group
@@ -640,15 +659,19 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             continue;
 #endif
             const uint64_t f0 = fp;
-            uint32_t acc = 0xFFFFFFFFu;
+            uint32_t acc = 0xFFFFFFFFu, accL = 0xFFFFFFFFu;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
 #pragma unroll
                 for (int k = 4 * q; k < 4 * q + 4; k += 2) {
                     fp = (fp << 1) + cg[k];
                     const uint32_t k0 = uint32_t(fp >> 32) & vhi;
+                    uint32_t l0 = 0;
+                    if constexpr (kFused) l0 = __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm;
                     fp = (fp << 1) + cg[k + 1];
                     acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
+                    if constexpr (kFused)
+                        accL = umin3(accL, l0, __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm);
                 }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -666,6 +689,10 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             if (acc == 0) [[unlikely]]
 #endif
                 recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
+            if constexpr (kFused) {
+                if (accL == 0) [[unlikely]]
+                    record_l_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, lws, vlm, recL);
+            }
         }
     };
     if (1 < TT) stage(C1{}, 1, Bv, A);
@@ -870,6 +897,10 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     }
 #endif
     if (s < int64_t(D.len)) (kMaskL ? W.runsL : W.runs)[64ull * D.task_base + seg0 + lane] = rec;
+    if constexpr (kFused) {
+        if (s < int64_t(D.len)) W.runsL[64ull * D.task_base + seg0 + lane] = recL;
+        if (lane == 0) W.validL[task] = 1u;
+    }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 }
 
@@ -881,6 +912,16 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const Dev
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan_l(const Batch B, const DevParams P, const Workspace W)
 {
     scan_body<true>(B, P, W);
+}
+
+// Both indexes in one pass (launched instead of k_scan + k_scan_l while the
+// adaptive hint says the MaskL index is needed): the MaskL key is a window of
+// the same fingerprint, one v_alignbit + v_and and half a v_min3 per byte.
+__global__ __launch_bounds__(kS2Waves * 64) void k_scan_f(const Batch B, const DevParams P, const Workspace W)
+{
+#if CDC_SCAN_V2
+    scan_body<false, true>(B, P, W);
+#endif
 }
 
 // DPP helpers (in-row lane shifts, no LDS round trip; ds_bpermute-based
@@ -2020,13 +2061,19 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     // With profiling on, the events ride on the kernels' own dispatch packets
     // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
     const dim3 sgrid((B.total_tasks + kS2Waves - 1) / kS2Waves), sblock(kS2Waves * 64);
+    const bool fused = CDC_SCAN_V2 && B.maskl_index && B.maskl_fused;  // k_scan_f: both indexes in one pass
     if (B.total_tasks == 0) {  // every buffer is empty
         if (prof) {
             (void)hipEventRecord(pr.e0, st);
             (void)hipEventRecord(pr.e1, st);
         }
     } else if (prof) {
-        hipExtLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
+        if (fused)
+            hipExtLaunchKernelGGL(k_scan_f, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
+        else
+            hipExtLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, pr.e0, pr.e1, 0, B, P, W);
+    } else if (fused) {
+        hipLaunchKernelGGL(k_scan_f, sgrid, sblock, 0, st, B, P, W);
     } else {
         hipLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, B, P, W);
     }
@@ -2045,7 +2092,8 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     }
     // MaskL index of the tasks near long MaskS-free stretches (most workgroups
     // exit after one look at the MaskS index on ordinary data)
-    if (B.total_tasks > 0 && B.maskl_index) hipLaunchKernelGGL(k_scan_l, sgrid, sblock, 0, st, B, P, W);
+    if (B.total_tasks > 0 && B.maskl_index && !fused)
+        hipLaunchKernelGGL(k_scan_l, sgrid, sblock, 0, st, B, P, W);
     if (B.total_segs > 0 && !B.force_fallback) {
         const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
         hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);

@@ -90,5 +90,6 @@ def set_debug_mode(mode):
 
 def set_maskl_index_mode(mode):
     """0 = never build the MaskL index, 1 = adaptive (default), 2 = every
-    launch group. Cut points do not depend on it."""
+    launch group in the fused pass (k_scan_f), 3 = every launch group by
+    k_scan_l. Cut points do not depend on it."""
     check(lib().cdc_set_maskl_index_mode(int(mode)))

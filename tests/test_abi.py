@@ -41,11 +41,11 @@ def test_abi_version_and_defaults():
 
 
 def test_maskl_index_mode_setter():
-    """Device-free knob: valid modes 0-2, anything else CDC_E_INVALID."""
+    """Device-free knob: valid modes 0-3, anything else CDC_E_INVALID."""
     L = _lib.lib()
-    assert L.cdc_set_maskl_index_mode(3) == _lib.CDC_E_INVALID
+    assert L.cdc_set_maskl_index_mode(4) == _lib.CDC_E_INVALID
     assert L.cdc_set_maskl_index_mode(-1) == _lib.CDC_E_INVALID
-    for m in (0, 2, 1):
+    for m in (0, 2, 3, 1):
         assert L.cdc_set_maskl_index_mode(m) == 0
 
 

@@ -55,12 +55,17 @@ def assert_same(got, ref, what=""):
     assert bad.size == 0, f"{what}: first mismatch at chunk {bad[0]}: {got[bad[0]]} vs {ref[bad[0]]}"
 
 
+# the suite's MaskL index mode (CDC_MASKL_INDEX, as the library reads it), restored after each test
+_MASKL_ENV = os.environ.get("CDC_MASKL_INDEX", "1")[:1]
+_MASKL_MODE = int(_MASKL_ENV) if _MASKL_ENV in ("0", "1", "2", "3") else 1
+
+
 @pytest.fixture(autouse=True)
 def _reset_debug():
     device.set_debug_mode(0)
     yield
     device.set_debug_mode(0)
-    device.set_maskl_index_mode(1)
+    device.set_maskl_index_mode(_MASKL_MODE)
     _lib.ensure_init(gear=_lib.default_gear())
 
 
@@ -155,12 +160,12 @@ def test_device_alternative_masks(oracle):
 
 
 # ---------------------------------------------------------------- MaskL index modes
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_maskl_index_modes(oracle, mode):
     """C3-like data (zeros + 1 % random bytes): a quarter of the chunks pass
     Normal and end on MaskL candidates. Never / adaptive / always building the
-    MaskL index (k_scan_l) gives the same cuts; several launches so adaptive
-    mode runs both with and without the index."""
+    MaskL index (2: in the fused pass k_scan_f, 3: by k_scan_l) gives the same
+    cuts; several launches so adaptive mode runs with and without the index."""
     data = low_entropy(48 << 20, 71)
     gear = _placeholder()
     ref = oracle.chunk(data, gear, **DEF)
