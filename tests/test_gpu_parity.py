@@ -176,6 +176,32 @@ def test_maskl_index_modes(oracle, mode):
         assert_same(got, ref, f"maskl mode {mode} rep {rep}")
 
 
+@pytest.mark.parametrize("masks", [
+    (0x0000000000001FFF, 0x00000000000001FF),  # MaskL inside MaskS's span: fused window exists
+    (0x0000000000001FFF, 0x00000000000301FF),  # MaskL's top bit above MaskS's: no fused window
+    (0x0003590703530000, 0x0000800000000001),  # MaskL spans 48 bits: no 32-bit window
+], ids=["fusable", "maskl-above", "maskl-wide"])
+@pytest.mark.parametrize("mode", [2, 3])
+def test_maskl_index_alternative_masks(oracle, masks, mode):
+    """The fused pass's MaskL window is derived from the masks; where none
+    exists, mode 2 falls back to k_scan + k_scan_l. At these sizes many
+    chunks pass Normal and end on MaskL candidates."""
+    ms, ml = masks
+    gear = gear_table(52)
+    _lib.ensure_init(gear=gear, mask_s=ms, mask_l=ml)
+    device.set_maskl_index_mode(mode)
+    p = dict(min_size=1024, normal_size=8192, max_size=32768)
+    data = random_bytes(4 << 20, 52)
+    ref = oracle.chunk(data, gear, mask_s=ms, mask_l=ml, **p)
+    assert (ref[:, 1] > p["normal_size"]).any(), "no chunk reaches the MaskL region"
+    t = torch.from_numpy(data).cuda()
+    for rep in range(2):
+        b = device.DeviceBatch([t], _opts(p))
+        b.launch()
+        (c,), _ = b.results()
+        assert_same(c.cpu().numpy().astype(np.uint64), ref, f"masks {ms:#x}/{ml:#x} mode {mode} rep {rep}")
+
+
 # ---------------------------------------------------------------- debug resolver
 @pytest.mark.parametrize("kind", ["random", "low_entropy"])
 def test_sequential_resolver_matches(oracle, kind):
