@@ -241,11 +241,10 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
     Workspace W;
     W.runs = reinterpret_cast<uint64_t *>(b + pl.off_runs);
     W.w1_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w1_nodes);
-    W.w1_cnt = reinterpret_cast<uint32_t *>(b + pl.off_w1_cnt);
-    W.w2_nodes = reinterpret_cast<uint64_t *>(b + pl.off_w2_nodes);
-    W.piece = reinterpret_cast<Piece *>(b + pl.off_piece);
+    W.xg = reinterpret_cast<uint64_t *>(b + pl.off_xg);
+    W.sg = reinterpret_cast<uint64_t *>(b + pl.off_sg);
     W.flags = reinterpret_cast<uint32_t *>(b + pl.off_flags);
-    W.w1_exit = reinterpret_cast<uint64_t *>(b + pl.off_w1_exit);
+    W.tick = reinterpret_cast<uint32_t *>(b + pl.off_tick);
     W.gear = gear;
     W.runsL = reinterpret_cast<uint64_t *>(b + pl.off_runsL);
     W.validL = reinterpret_cast<uint32_t *>(b + pl.off_validL);
@@ -267,8 +266,6 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     B.final_ = final_ ? 1u : 0u;
     B.total_segs = pl.total_segs;
     B.total_tasks = pl.total_tasks;
-    B.cap1 = pl.cap1;
-    B.cap2 = pl.cap2;
     B.seg = pl.seg;
     B.scan_lane = pl.scan_lane;
     static const uint32_t dbg = [] {

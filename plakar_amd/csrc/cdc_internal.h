@@ -19,7 +19,7 @@ constexpr int kMaxBufsPerLaunch = 32;   // buffers per launch group (kernel-arg 
 // "dense": walkers rescan its bytes.
 constexpr uint32_t kRunCap = 3;
 constexpr uint32_t kMaxScanLane = 65536;  // run offsets are u16
-constexpr uint32_t kMaxSegs = 16384;    // resolution segments per buffer
+constexpr uint32_t kMaxSegs = 1u << 22; // resolution segments per buffer (seg grows past 32 Min beyond)
 constexpr uint32_t kScanLaneBytes = 16384;  // max bytes hashed+tested per scan lane (multiple of 256)
 #ifndef CDC_WALK_WAVES
 #define CDC_WALK_WAVES 4
@@ -59,7 +59,6 @@ struct Batch {
     uint32_t nbufs;
     uint32_t final_;
     uint32_t total_segs, total_tasks;
-    uint32_t cap1, cap2;     // per-segment node capacities (speculative / junction walks)
     uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
     uint32_t scan_lane;      // bytes per scan lane (= per index run); one wave (scan task) = 64 lanes
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
@@ -70,28 +69,16 @@ struct Batch {
     BufDesc b[kMaxBufsPerLaunch];
 };
 
-// The piece of the true chain that segment q contributes when the chain enters
-// it through its junction (q >= 1) or at offset 0 (q == 0): the c2 junction
-// nodes, then the speculative nodes of segment `conv` from index k on; cnt
-// nodes in all, and `end` is the node after the last one (the piece's exit).
-struct Piece {
-    uint32_t conv;  // local segment the junction walk merged into, or kConv*
-    uint32_t c2;    // junction-walk nodes (w2_nodes)
-    uint32_t k;     // merge index in segment conv's speculative chain
-    uint32_t cnt;   // nodes in the piece
-    uint64_t end;   // exit node (kUndet: undecided)
-    uint64_t pad;
-};
-
 // Device workspace, carved out of one caller-provided allocation.
 struct Workspace {
     uint64_t *runs;      // [total_tasks * 64] candidate-index records (run q of buffer b at 64 * task_base + q)
-    uint64_t *w1_nodes;  // [total_segs * cap1] speculative chain per segment
-    uint32_t *w1_cnt;    // [total_segs]
-    uint64_t *w2_nodes;  // [total_segs * cap2] junction walk per segment
-    Piece *piece;        // [total_segs] what segment q contributes if the true chain enters it
-    uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "needs sequential fallback"
-    uint64_t *w1_exit;   // [total_segs] last node of the speculative chain (its exit)
+    // k_resolve's per-segment words (see cdc_kernels.hip); xg and sg are
+    // zeroed by the scan kernel of the same launch group.
+    uint64_t *w1_nodes;  // [total_segs * 64] speculative chain of each segment
+    uint64_t *xg;        // [total_segs] granule: published | node count | speculative exit X_q
+    uint64_t *sg;        // [total_segs] granule: LOCAL (conv, cuts) or INCLUSIVE (E, O)
+    uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "resolve sequentially"
+    uint32_t *tick;      // [2] workgroup ticket (dispatch order)
     const uint64_t *gear;  // 256 entries, device copy
     // MaskL candidate index (same record format as runs), built by k_scan_l
     // only for the scan tasks near a long MaskS-free stretch; validL[task]
@@ -100,17 +87,12 @@ struct Workspace {
     uint32_t *validL;    // [total_tasks]
 };
 
-constexpr uint32_t kConvNone = 0xFFFFFFFFu;  // entry was already terminal (chain ended earlier)
-constexpr uint32_t kConvTerm = 0xFFFFFFFEu;  // chain ended inside this junction walk
-constexpr uint32_t kConvOvf = 0xFFFFFFFDu;   // junction walk exceeded cap2 nodes
-
 struct Plan {
     uint64_t seg;
     uint32_t scan_lane;
-    uint32_t cap1, cap2;
     uint32_t total_segs, total_tasks;
-    size_t off_runs, off_w1_nodes, off_w1_cnt, off_w2_nodes, off_piece, off_flags,
-        off_w1_exit, off_runsL, off_validL, bytes;
+    size_t off_runs, off_w1_nodes, off_xg, off_sg, off_flags, off_tick, off_runsL, off_validL,
+        bytes;
 };
 
 // Host-side helpers implemented in cdc_kernels.hip.

@@ -12,16 +12,14 @@
 //               depend on the last W <= 64 bytes), tests MaskS at every
 //               position and appends the rare hits to a candidate index of
 //               64-KiB blocks (u16 offsets).
-//   k_walk1     speculative chains: one wave per resolution segment, walking
-//               next() from the segment start (a guess) across the segment.
-//   k_walk2     junctions: one wave per segment walks the TRUE chain from the
-//               previous segment's exit until it meets a speculative chain.
-//   k_emit      one workgroup per buffer: selects the junction walks that lie
-//               on the chain from offset 0, prefix-sums and writes the
-//               (offset, length) cut list; flags a buffer whose chains
-//               never merged (pathological data).
-//   k_seq       sequential single-wave walk for flagged buffers (and every
-//               buffer in the cross-check debug mode); exits at once otherwise.
+//   k_resolve   the chain of cuts, one wave per resolution segment, in one
+//               launch: a speculative chain from the segment start (walked
+//               through a successor graph of the segment's candidates built
+//               lane-parallel in LDS), the junction from the previous
+//               segment's speculative exit, a decoupled look-back for the
+//               true entry and the cut offset, then the cut list and the
+//               result row.  Pathological data (and the debug mode) fall back
+//               to a sequential single-wave walk of the buffer.
 //
 // next(p) is wave-cooperative and decides exactly what the reference decides:
 // the truncated window [p+Min, p+Min+W-1) (fingerprint reset at p+Min) by a
@@ -44,7 +42,6 @@ static constexpr uint64_t kNoHit = ~0ull;
 #endif
 static constexpr uint32_t kRawLaneBytes = CDC_RAW_LANE;  // bytes tested per lane per raw-scan block
 static constexpr uint32_t kWarm = 64;           // warm-up bytes (>= W - 1 for any mask)
-static constexpr uint32_t kNtCap = 4096;        // emit: non-trivial junctions per buffer
 
 // ---------------------------------------------------------------------------
 // Gear table in LDS: 256 entries x 32 copies, 256 B per entry.  Lane l reads
@@ -211,11 +208,10 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t x)
 // boundaries, read back with cdc_debug_timestamps().  Off in production.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kDbgTs = 16;
+constexpr uint32_t kDbgGraph = 32;  // with kDbgTs: k_resolve slots 5-7 time graph_build's phases
 constexpr uint32_t kTsScan = 0;                       // 4 per scan workgroup (<= 4096)
-constexpr uint32_t kTsW1 = kTsScan + 4 * 4096;        // 8 per segment
-constexpr uint32_t kTsW2 = kTsW1 + 8 * kMaxSegs;      // 8 per segment
-constexpr uint32_t kTsEmit = kTsW2 + 8 * kMaxSegs;    // 16 for buffer 0
-constexpr uint32_t kTsSlots = kTsEmit + 16;
+constexpr uint32_t kTsRes = kTsScan + 4 * 4096;       // 8 per resolution segment (<= 16384)
+constexpr uint32_t kTsSlots = kTsRes + 8 * 16384;
 __device__ uint64_t g_ts[kTsSlots];
 
 __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
@@ -530,7 +526,16 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
         if (threadIdx.x == 0 && B.maskl_hint)
             __hip_atomic_store(B.maskl_hint, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
+    if constexpr (!kMaskL) {  // k_resolve's per-segment status words and tickets of this launch group
+        const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+        for (uint32_t i = gt; i < B.total_segs; i += nth) {
+            W.xg[i] = 0ull;
+            W.sg[i] = 0ull;
+        }
+        if (gt < kMaxBufsPerLaunch) W.flags[gt] = 0u;
+        if (gt < 2) W.tick[gt] = 0u;
+        if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
+    }
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, kMaskL ? P.fl_sh : P.fs_sh);
     __syncthreads();
     if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
@@ -1300,68 +1305,33 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
 }
 
 // ---------------------------------------------------------------------------
-// Speculative walking.  On ordinary data next(p) is "the first full-window
-// MaskS candidate in [p + Min + W - 1, p + Normal)" + cut_adj: a hit in the
-// truncated window (the W - 1 positions after p + Min, fingerprint reset
-// there) has probability ~(W - 1) 2^-15 per node.  So a walk
-//   1. preloads the candidate-index blocks it can reach into wave-local LDS
-//      (one global round trip),
-//   2. follows candidate-only successors through LDS for up to kSpecK nodes,
-//   3. loads the truncated-window bytes of all those nodes at once (one round
-//      trip) and verifies them in order: the first node whose truncated window
-//      hits takes that hit as its successor, and the next round starts there.
-// A step the preload cannot answer (a dense index block, a reach beyond the
-// preloaded blocks, the MaskL region, the last Min bytes of the buffer) takes
-// the exact next_node().  Results are identical to next_node() step by step.
+// Successor graph of a resolution segment (k_resolve).
+//
+// On ordinary data next(v) is the first full-window MaskS candidate in
+// [v + Min + W - 1, v + Normal), plus cut_adj, unless the truncated window
+// [v + Min, v + Min + W - 1) hits first.  So nearly every chunk start a walk
+// visits is a "listed" node v = c + cut_adj of a stored candidate c.  A
+// walker wave lists the nodes of its segment (at most kGNodes, two per lane)
+// and every lane computes the successors of its own nodes at once: the
+// truncated window rolled lane-serially from 17 dwords, the full-window
+// search over the segment's run records preloaded into LDS (one round trip,
+// with a 1-bit-per-run "holds a candidate" map to skip empty runs).  A node
+// whose successor needs more (a dense run whose stored entries do not answer,
+// the MaskL region, a clipped or end-of-buffer window, records beyond the
+// preload) is kGHard: there the walk takes the exact next_node().  The walk
+// then reads each listed node's successor (position and list index) with
+// readlane, a few cycles per chunk instead of a global round trip.
 // ---------------------------------------------------------------------------
-#ifndef CDC_WALK_SPEC
-#define CDC_WALK_SPEC 0
-#endif
-constexpr uint32_t kSpecK = 16;      // nodes speculated per round
-constexpr uint32_t kPreRuns = 1024;  // index runs preloaded per wave (8 KiB of LDS)
-static constexpr uint64_t kSpecMiss = ~1ull;
+constexpr uint32_t kGNodes = 128;      // listed nodes per segment (two per lane)
+constexpr uint32_t kGRecs = 512;       // run records preloaded per wave
+constexpr uint64_t kGHard = ~1ull;     // successor not decided by the graph
+constexpr uint32_t kGNone = 0xFFFFu;   // not a listed node
 
-struct SpecIdx {
-    uint64_t *rec;  // LDS [kPreRuns]
-    uint64_t r0;    // first preloaded run
-    uint32_t nr;    // preloaded runs
+struct GraphLds {
+    uint64_t rec[kGRecs];        // runs ra .. ra + nr - 1
+    uint64_t bits[kGRecs / 64];  // bit i: run ra + i holds a candidate (dense included)
+    uint64_t node[kGNodes];      // listed nodes, ascending
 };
-
-// Preload the run records covering [a, b) (clipped to the buffer and kPreRuns).
-__device__ void spec_preload(const WalkCtx &C, SpecIdx &S, uint64_t a, uint64_t b)
-{
-    S.nr = 0;
-    S.r0 = 0;
-    if (b > C.len) b = C.len;
-    if (a >= b) return;
-    S.r0 = run_of(C, a);
-    const uint64_t rl = run_of(C, b - 1);
-    const uint32_t nr = uint32_t(min<uint64_t>(rl - S.r0 + 1, kPreRuns));
-    for (uint32_t i = C.lane; i < nr; i += 64) S.rec[i] = C.runs[S.r0 + i];
-    S.nr = nr;
-}
-
-// First candidate in [a, b) from the preload; kNoHit if there is none,
-// kSpecMiss if the preload cannot tell (runs outside it, a dense run first).
-__device__ uint64_t spec_first(const WalkCtx &C, const SpecIdx &S, uint64_t a, uint64_t b)
-{
-    const uint64_t rl = run_of(C, b - 1);
-    for (uint64_t r = run_of(C, a); r <= rl; r += 64) {
-        const uint64_t ri = r + C.lane;
-        const bool want = ri <= rl;
-        const uint64_t li = ri - S.r0;
-        if (__ballot(want && (ri < S.r0 || li >= S.nr))) return kSpecMiss;
-        const uint64_t rec = want ? S.rec[li] : 0ull;
-        const uint64_t cand = want ? rec_first(rec, ri * C.sl, a, b) : kNoHit;
-        const uint64_t mc = __ballot(cand != kNoHit);
-        const uint64_t md = __ballot(want && cand == kNoHit && (rec & 0xFFFFu) > kRunCap);
-        const int lf = mc ? __ffsll((unsigned long long)mc) - 1 : 64;
-        const int ld = md ? __ffsll((unsigned long long)md) - 1 : 64;
-        if (ld < lf) return kSpecMiss;
-        if (lf < 64) return readlane64(cand, lf);
-    }
-    return kNoHit;
-}
 
 // The chunk window next_node() works on for a chunk starting at p (r > Min).
 struct ChunkWin {
@@ -1387,72 +1357,189 @@ __device__ __forceinline__ ChunkWin chunk_win(const WalkCtx &C, const DevParams 
     return ChunkWin{p + P.min_size, p + norm, lim};
 }
 
-// Candidate-only successor of x (its truncated window still to verify), or
-// kSpecMiss when the preload cannot answer (the caller then takes next_node).
-__device__ __forceinline__ uint64_t spec_cand(const WalkCtx &C, const DevParams &P, const SpecIdx &S, uint64_t x)
+// next_node(v) computed by ONE lane from the preloaded records, or kGHard.
+// Identical to next_node() wherever it does not return kGHard.
+__device__ __forceinline__ uint64_t graph_succ(const WalkCtx &C, const DevParams &P, const GraphLds &L, uint64_t ra,
+                                               uint32_t nr, uint64_t v)
 {
-    if (C.len - x <= P.min_size) return kSpecMiss;
-    const ChunkWin w = chunk_win(C, P, x);
-    const uint64_t full0 = w.fz + (P.win - 1);
+    const uint64_t E = C.len;
+    if (v >= E || E - v <= P.min_size) return kGHard;      // last chunk: next_node decides
+    if (!C.final_ && v + P.max_size > E) return kGHard;    // clipped window (kUndet or a cut)
+    const ChunkWin w = chunk_win(C, P, v);
+    const uint64_t fz = w.fz, full0 = fz + (P.win - 1);
+    if (w.norm_end < full0 || w.lim < full0) return kGHard;  // truncated window not all MaskS / in range
+    // ---- truncated window [fz, full0): fingerprint from 0 at fz, MaskS at every position
+    const uint64_t a = C.ub + fz;
+    const uint64_t a4 = a & ~3ull, last = (C.ub + E - 1) & ~3ull;  // full0 <= E: the used dwords are in bounds
+    const uint32_t sh = uint32_t(a & 3u);
+    uint32_t dw[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) dw[k] = *reinterpret_cast<const uint32_t *>(min<uint64_t>(a4 + 4u * uint64_t(k), last));
+    const uint32_t wm1 = P.win - 1;  // positions tested (<= 63)
+    uint64_t fp = 0;
+    uint32_t first = 63;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t word = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+        uint64_t gq[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) gq[t] = lds_gear(C.tab, wgear_addr(C.laneoff, word, t));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t j = uint32_t(4 * k + t);
+            if (j >= 63) break;
+            fp = (fp << 1) + gq[t];
+            const bool hit = key_of(fp, P.ms_lo, P.ms_hi) == 0 && j < wm1;
+            first = min(first, hit ? j : 63u);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // 4 gathers in flight at a time: bounded registers
+    }
+    if (first < wm1) return fz + first + P.cut_adj;
+    // ---- full-window MaskS candidates in [full0, s_end) from the records
     const uint64_t s_end = min(w.norm_end, w.lim);
-    if (full0 >= s_end) return kSpecMiss;
-    const uint64_t q = spec_first(C, S, full0, s_end);
-    return (q == kNoHit || q == kSpecMiss) ? kSpecMiss : q + P.cut_adj;
+    if (full0 < s_end) {
+        const uint64_t rl = run_of(C, s_end - 1);
+        uint64_t r = run_of(C, full0);
+        for (;;) {
+            if (r > rl) break;  // no candidate
+            uint64_t i = r - ra;
+            if (i >= nr) return kGHard;
+            uint32_t wd = uint32_t(i >> 6);
+            uint64_t bits = L.bits[wd] & (~0ull << (i & 63u));
+            while (!bits) {
+                ++wd;
+                if (uint64_t(wd) * 64u >= nr) break;
+                bits = L.bits[wd];
+            }
+            if (!bits) {
+                if (ra + nr > rl) break;  // the preload covers the rest: no candidate
+                return kGHard;
+            }
+            i = uint64_t(wd) * 64u + uint64_t(__builtin_ctzll(bits));
+            r = ra + i;
+            if (r > rl) break;
+            const uint64_t rec = L.rec[i];
+            const uint64_t cand = rec_first(rec, r * C.sl, full0, s_end);
+            if (cand != kNoHit) return cand + P.cut_adj;
+            if ((rec & 0xFFFFu) > kRunCap) return kGHard;  // dense: the stored entries do not answer
+            ++r;
+        }
+    }
+    if (max(w.norm_end, full0) < w.lim) return kGHard;  // MaskL region: index or raw scan
+    return w.lim;                                        // forced cut at v + n
 }
 
-// Wave-local LDS scratch of one speculative round.
-struct SpecBuf {
-    uint64_t x[kSpecK];    // node
-    uint64_t nx[kSpecK];   // its successor
-    uint32_t ex[kSpecK];   // 1: nx is next_node()'s (exact), 0: candidate-only
-    uint8_t byt[kSpecK][64];
-    uint64_t t_spec;       // debug: s_memrealtime after the speculation loop
+// The segment's listed nodes and their successors, held two per lane.
+struct Graph {
+    uint32_t n;       // listed nodes (> kGNodes: overflow, graph unused)
+    uint64_t v[2];    // node lane (+ 64 s)
+    uint64_t sp[2];   // its successor, or kGHard
+    uint32_t si[2];   // the successor's list index, or kGNone
 };
 
-// One speculative round from x: up to kSpecK verified successors in R.nx[0..n),
-// stopping after the first one that is kUndet, >= len or >= stop.  Returns n.
-__device__ uint32_t spec_round(const WalkCtx &C, const DevParams &P, const SpecIdx &S, uint64_t x, uint64_t stop,
-                               SpecBuf &R)
+__device__ __forceinline__ uint32_t graph_find(const GraphLds &L, uint32_t n, uint64_t x)
 {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.node[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && L.node[lo] == x ? lo : kGNone;
+}
+
+// Wave-uniform list index of node x, or kGNone.
+__device__ __forceinline__ uint32_t graph_lookup(const Graph &G, uint32_t lane, uint64_t x)
+{
+    if (G.n > kGNodes) return kGNone;
+    const uint64_t m0 = __ballot(lane < G.n && G.v[0] == x);
+    if (m0) return uint32_t(__ffsll((unsigned long long)m0) - 1);
+    const uint64_t m1 = __ballot(lane + 64u < G.n && G.v[1] == x);
+    return m1 ? 64u + uint32_t(__ffsll((unsigned long long)m1) - 1) : kGNone;
+}
+
+// Build the graph of segment [S0, S1): list, preload, successors.
+__device__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, Graph &G, uint64_t S0, uint64_t S1,
+                            const Batch &B, uint32_t tslot)
+{
+    const bool tg = (B.debug & kDbgGraph) && C.lane == 0;
+    const uint32_t lane = C.lane;
+    const uint64_t adj = P.cut_adj;
+    const uint64_t clo = S0 >= adj ? S0 - adj : 0, chi = S1 - adj;  // candidates c with c + adj in [S0, S1)
+    const uint64_t ra = run_of(C, clo);
+    const uint64_t rneed = run_of(C, min(C.len, S1 + P.normal_size) - 1);
+    const uint32_t nr = uint32_t(min<uint64_t>(rneed - ra + 1, kGRecs));
+    uint64_t recs[kGRecs / 64];
+#pragma unroll
+    for (uint32_t k = 0; k < kGRecs / 64; ++k) {
+        const uint32_t i = 64u * k + lane;
+        recs[k] = 64u * k < nr && i < nr ? C.runs[ra + i] : 0ull;
+    }
     uint32_t n = 0;
-    for (uint64_t y = x; n < kSpecK;) {
-        uint64_t q = spec_cand(C, P, S, y);
-        const bool exact = q == kSpecMiss;
-        if (exact) q = next_node(C, P, y);
-        if (C.lane == 0) {
-            R.x[n] = y;
-            R.nx[n] = q;
-            R.ex[n] = exact ? 1u : 0u;
-        }
-        ++n;
-        if (q == kUndet || q >= C.len || q >= stop) break;
-        y = q;
-    }
-    if (C.lane == 0) R.t_spec = __builtin_amdgcn_s_memrealtime();
-    // the truncated-window bytes of every speculated node, in one round trip
-    const uint8_t *data = reinterpret_cast<const uint8_t *>(C.ub);
-    uint32_t byt[kSpecK];
+    const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (uint32_t k = 0; k < kSpecK; ++k) {
-        byt[k] = 0;
-        if (k < n && !R.ex[k]) {
-            const ChunkWin w = chunk_win(C, P, R.x[k]);
-            const uint64_t pos = w.fz + C.lane;
-            if (C.lane + 1 < P.win && pos < w.lim) byt[k] = data[pos];
-        }
-    }
+    for (uint32_t k = 0; k < kGRecs / 64; ++k) {
+        if (64u * k >= nr) break;
+        const uint32_t i = 64u * k + lane;
+        const uint64_t rec = recs[k];
+        if (i < nr) L.rec[i] = rec;
+        const uint64_t nb = __ballot(i < nr && (rec & 0xFFFFu) != 0);
+        if (lane == 0) L.bits[k] = nb;
+        // stored entries with c in [clo, chi): a contiguous range of the (ascending) entries
+        const uint64_t rs = (ra + i) * C.sl;
+        const uint32_t cnt = i < nr ? min(uint32_t(rec & 0xFFFFu), kRunCap) : 0u;
+        uint32_t e0 = 3, e1 = 0;  // listed entries [e0, e1)
 #pragma unroll
-    for (uint32_t k = 0; k < kSpecK; ++k) R.byt[k][C.lane] = uint8_t(byt[k]);
-    for (uint32_t k = 0; k < n; ++k) {
-        if (R.ex[k]) continue;
-        const ChunkWin w = chunk_win(C, P, R.x[k]);
-        const uint64_t h = trunc_first_hit(C, P, w.fz, w.norm_end, w.lim, R.byt[k][C.lane]);
-        if (h != kNoHit) {
-            if (C.lane == 0) R.nx[k] = h + P.cut_adj;
-            return k + 1;
+        for (uint32_t e = 0; e < kRunCap; ++e) {
+            const uint64_t c = rs + ((rec >> (16 + 16 * e)) & 0xFFFFu);
+            if (e < cnt && c >= clo && c < chi) {
+                e0 = min(e0, e);
+                e1 = e + 1;
+            }
+        }
+        const uint32_t kk = e1 > e0 ? e1 - e0 : 0u;
+        const uint64_t b0 = __ballot(kk & 1u), b1 = __ballot(kk & 2u);
+        const uint32_t pre = uint32_t(__popcll(b0 & below) + 2 * __popcll(b1 & below));
+#pragma unroll
+        for (uint32_t e = 0; e < kRunCap; ++e) {
+            const uint32_t o = n + pre + (e - e0);
+            if (e >= e0 && e < e1 && o < kGNodes) L.node[o] = rs + ((rec >> (16 + 16 * e)) & 0xFFFFu) + adj;
+        }
+        n += uint32_t(__popcll(b0) + 2 * __popcll(b1));
+    }
+    for (uint32_t k = (nr + 63) / 64; k < kGRecs / 64; ++k)
+        if (lane == 0) L.bits[k] = 0;
+    G.n = n;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, read back by other lanes
+    if (tg) dbg_ts(B, tslot + 5);
+    if (n > kGNodes) return;
+#pragma unroll 1
+    for (uint32_t s = 0; s < 2; ++s) {
+        if (64u * s >= n) break;
+        const uint32_t i = 64u * s + lane;
+        uint64_t v = kGHard, sp = kGHard;
+        uint32_t si = kGNone;
+        if (i < n) {
+            v = L.node[i];
+            sp = graph_succ(C, P, L, ra, nr, v);
+            if (sp != kGHard && sp >= S0 && sp < S1) si = graph_find(L, n, sp);
+        }
+        if (tg) dbg_ts(B, tslot + 6 + s);
+        if (s == 0) {
+            G.v[0] = v;
+            G.sp[0] = sp;
+            G.si[0] = si;
+        } else {
+            G.v[1] = v;
+            G.sp[1] = sp;
+            G.si[1] = si;
         }
     }
-    return n;
+    if (n <= 64) {
+        G.v[1] = kGHard;
+        G.sp[1] = kGHard;
+        G.si[1] = kGNone;
+    }
 }
 
 __device__ __forceinline__ uint32_t buf_of_seg(const Batch &B, uint32_t g)
@@ -1485,460 +1572,431 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
 }
 
 // ---------------------------------------------------------------------------
-// k_walk1: speculative chain per segment, started at the segment start.
+// k_resolve: the chain resolution of every buffer of a launch group in ONE
+// launch, one wave per resolution segment [S0, S1) (B.seg bytes, the last one
+// clipped to the buffer).
+//
+//   A. Speculative chain: the walk from S0 (a guess) to the first node >= S1
+//      (through the segment's successor graph, next_node() where the graph
+//      cannot answer).  Its nodes (w1_nodes) and exit X_q are published at
+//      once (granule xg); this phase never waits.
+//   B. Junction: the true chain enters segment q at X_{q-1} when segment q - 1
+//      is on it.  The wave walks from X_{q-1} until it lands on a node of some
+//      segment's speculative chain (its own, or a later one's, published in
+//      phase A): it merged into segment conv >= q, so segments q+1 .. conv are
+//      skipped and the next piece starts at X_conv, exactly the entry that
+//      segment conv + 1 assumed.  Published as LOCAL (conv, cut count).
+//   C. Decoupled look-back over the lower segments of the buffer for E, the
+//      next segment on the true chain, and O, the cuts before it.  A LOCAL
+//      with conv == its own index ("trivial") composes by addition; the first
+//      non-trivial LOCAL met is waited on until it is INCLUSIVE.
+//   D. If q is on the chain (E == q), its piece's cuts are written at O; then
+//      the INCLUSIVE status (E_q, O_q) is published.  The buffer's last
+//      segment writes the result row.
+//
+// Hand-offs are 8-byte granules (tag + data) written by ONE relaxed agent
+// store (sc1) and polled with relaxed agent loads: no fences, no acquire
+// polls (MI355X_MICROARCH.md, visibility).  A wave waits on lower segments,
+// and on higher segments' phase-A publications only; workgroups take their
+// segments in dispatch order (a ticket), so everything waited on is running
+// or will be dispatched once some wave finishes: no deadlock whatever the
+// grid size.  Node lists live in registers (node i of a list in lane i); a
+// junction walk longer than 64 nodes (chains that never merge), and the debug
+// mode, flag the buffer: its last segment waits for every INCLUSIVE status of
+// the buffer and resolves it by the sequential walk.  Cut rows are stored
+// write-through, so the sequential rewrite is the last word.  The granules
+// are zeroed by the scan kernel of the same launch group.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk1(const Batch B, const DevParams P,
-                                                               const Workspace W)
+constexpr uint32_t kMaxList = 64;                // nodes per register list
+constexpr uint64_t kX56 = (1ull << 56) - 1;      // xg: X in bits 0-55 (all ones: kUndet)
+constexpr uint64_t kKindLocal = 1ull << 62, kKindIncl = 2ull << 62;
+constexpr uint32_t kConvEnd = 0x3FFFFFu;         // LOCAL: the chain ends in this piece (or before it)
+constexpr uint32_t kSegEnd = 0xFFFFFFu;          // INCLUSIVE: no further segment on the chain
+
+__device__ __forceinline__ uint64_t ld_rlx(const uint64_t *p)
 {
-    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
-    __shared__ uint64_t s_tab[256 * kWCopies];
-#if CDC_RAW_TAB32
-    __shared__ uint64_t s_tab32[256 * 32];
-    __shared__ uint32_t s_tab32_ready;
-    if (threadIdx.x == 0) s_tab32_ready = 0u;
-#define CDC_TAB32_ARGS , s_tab32, &s_tab32_ready
-#else
-#define CDC_TAB32_ARGS
-#endif
-#if CDC_WALK_SPEC
-    __shared__ uint64_t s_prec[kWalkWavesPerWG][kPreRuns];
-    __shared__ SpecBuf s_spec[kWalkWavesPerWG];
-#endif
-    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
-    const bool l0 = (threadIdx.x & 63u) == 0;
-    if (l0) dbg_ts(B, kTsW1 + 8 * g);
-    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
-    __syncthreads();
-    if (l0) dbg_ts(B, kTsW1 + 8 * g + 1);
-    if (g >= B.total_segs) return;
-    const uint32_t b = buf_of_seg(B, g);
-    const BufDesc &D = B.b[b];
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab) CDC_TAB32_ARGS);
-    const uint64_t q = g - D.seg_base;
-    const uint64_t seg_end = (q + 1) * B.seg;
-    uint64_t *nodes = W.w1_nodes + size_t(g) * B.cap1;
-    uint64_t p = q * B.seg;
-    uint32_t c = 0;
-    if (C.lane == 0) nodes[c] = p;
-    ++c;
-    uint64_t nx = p;
-#if CDC_WALK_SPEC
-    SpecIdx S;
-    S.rec = s_prec[threadIdx.x >> 6];
-    spec_preload(C, S, p + P.min_size, seg_end + P.max_size);
-    if (C.lane == 0) dbg_ts(B, kTsW1 + 8 * g + 2);
-    SpecBuf &R = s_spec[threadIdx.x >> 6];
-    for (uint32_t round = 0, done = 0; !done; ++round) {
-        const uint32_t n = spec_round(C, P, S, p, seg_end, R);
-        if (C.lane == 0 && round == 0) {
-            dbg_ts(B, kTsW1 + 8 * g + 5, __builtin_amdgcn_s_memrealtime());
-            dbg_ts(B, kTsW1 + 8 * g + 7, R.t_spec);
-        }
-        if (C.lane == 0) dbg_ts(B, kTsW1 + 8 * g + 6, round + 1);
-        for (uint32_t k = 0; k < n; ++k) {
-            nx = R.nx[k];
-            if (C.lane == 0) nodes[c] = nx;
-            ++c;
-            if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) {
-                done = 1;
-                break;
-            }
-        }
-        p = nx;
-    }
-#else
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void st_rlx(uint64_t *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void drain_stores()
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Poll a granule (every lane the same word) until it is non-zero.
+__device__ __forceinline__ uint64_t wait_granule(const uint64_t *p)
+{
     for (;;) {
-        nx = next_node(C, P, p);
-        if (C.lane == 0) nodes[c] = nx;
-        ++c;
-        if (nx == kUndet || nx >= C.len || nx >= seg_end || c >= B.cap1) break;
-        p = nx;
-    }
-#endif
-    if (C.lane == 0) {
-        W.w1_cnt[g] = c;
-        W.w1_exit[g] = nx;
-        if (q == 0) {  // the true chain starts here: the whole speculative chain is its piece
-            Piece pc;
-            pc.conv = 0;
-            pc.c2 = 0;
-            pc.k = 0;
-            pc.cnt = c - 1;
-            pc.end = nx;
-            pc.pad = 0;
-            W.piece[g] = pc;
-        }
-        dbg_ts(B, kTsW1 + 8 * g + 3);
-        dbg_ts(B, kTsW1 + 8 * g + 4, c);
+        const uint64_t v = readlane64(ld_rlx(p), 0);
+        if (v) return v;
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_walk2: junction walk from the previous segment's exit until the chain
-// meets a node of some segment's speculative chain.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_WALK_ATTR void k_walk2(const Batch B, const DevParams P,
-                                                               const Workspace W)
+__device__ __forceinline__ uint64_t x_dec(uint64_t g) { return (g & kX56) == kX56 ? kUndet : (g & kX56); }
+__device__ __forceinline__ uint64_t x_enc(uint64_t x, uint32_t ns)
 {
-    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
-    __shared__ uint64_t s_tab[256 * kWCopies];
-#if CDC_RAW_TAB32
-    __shared__ uint64_t s_tab32[256 * 32];
-    __shared__ uint32_t s_tab32_ready;
-    if (threadIdx.x == 0) s_tab32_ready = 0u;
-#define CDC_TAB32_ARGS , s_tab32, &s_tab32_ready
-#else
-#define CDC_TAB32_ARGS
-#endif
-    const uint32_t g = blockIdx.x * kWalkWavesPerWG + (threadIdx.x >> 6);
-    const bool l0 = (threadIdx.x & 63u) == 0;
-    if (l0) dbg_ts(B, kTsW2 + 8 * g);
-    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
-    __syncthreads();
-    if (l0) dbg_ts(B, kTsW2 + 8 * g + 1);
-    if (g >= B.total_segs) return;
-    const uint32_t b = buf_of_seg(B, g);
-    const BufDesc &D = B.b[b];
-    if (g == D.seg_base) return;  // segment 0 of a buffer has no junction
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab) CDC_TAB32_ARGS);
-    const uint32_t cap1 = B.cap1;
-    const uint64_t e = W.w1_exit[g - 1];
-    if (l0) dbg_ts(B, kTsW2 + 8 * g + 2, e);
-    uint32_t conv = kConvNone, idx = 0, c2 = 0, mcnt = 0;
-    uint64_t term = e, mend = 0;
-    uint64_t *out = W.w2_nodes + size_t(g) * B.cap2;
-    if (e != kUndet && e < C.len) {
-        uint64_t x = e;
-        for (;;) {
-            const uint64_t s = x / B.seg;
-            const uint32_t gs = D.seg_base + uint32_t(s);
-            const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
-            // the count and the first 64 speculative nodes in one round trip
-            const uint32_t ns = W.w1_cnt[gs] - 1;  // speculative nodes below the segment exit
-            const uint64_t gx = W.w1_exit[gs];
-            const uint64_t v0 = C.lane < cap1 ? sn[C.lane] : kUndet;
-            int k = -1;
-            {
-                const uint64_t m = __ballot(C.lane < ns && v0 == x);
-                if (m) k = __ffsll((unsigned long long)m) - 1;
-            }
-            for (uint32_t base = 64; base < ns && k < 0; base += 64) {
-                const uint32_t i = base + C.lane;
-                const uint64_t m = __ballot(i < ns && sn[i] == x);
-                if (m) k = int(base) + __ffsll((unsigned long long)m) - 1;
-            }
-            if (k >= 0) {
-                conv = uint32_t(s);
-                idx = uint32_t(k);
-                mcnt = ns - uint32_t(k);
-                mend = gx;
-                break;
-            }
-            if (c2 >= B.cap2) {
-                conv = kConvOvf;
-                break;
-            }
-            if (C.lane == 0) out[c2] = x;
-            ++c2;
-            x = next_node(C, P, x);
-            if (x == kUndet || x >= C.len) {
-                conv = kConvTerm;
-                term = x;
-                break;
-            }
-        }
-    }
-    if (C.lane == 0) {
-        Piece pc;
-        pc.conv = conv;
-        pc.c2 = c2;
-        pc.k = idx;
-        pc.pad = 0;
-        if (conv < kConvOvf) {  // merged: junction nodes, then the speculative chain from k
-            pc.cnt = c2 + mcnt;
-            pc.end = mend;
-        } else if (conv == kConvTerm) {  // the chain ended inside the junction walk
-            pc.cnt = c2;
-            pc.end = term;
-        } else {  // kConvNone: the chain ended before this segment; kConvOvf: fallback
-            pc.cnt = 0;
-            pc.end = term;
-        }
-        W.piece[g] = pc;
-        dbg_ts(B, kTsW2 + 8 * g + 3);
-        dbg_ts(B, kTsW2 + 8 * g + 4, c2);
-    }
+    return (1ull << 63) | (uint64_t(ns) << 56) | (x == kUndet || x >= kX56 ? kX56 : x);
 }
 
-// ---------------------------------------------------------------------------
-// k_seq: sequential resolver, one workgroup per buffer.  The workgroup fills
-// the Gear table, then wave 0 walks next() from offset 0 and writes the cut
-// list.  It runs only for buffers k_emit flagged: pathological data whose
-// speculative chains never merge, and the debug mode that cross-checks the fast
-// path.  A separate kernel so that k_emit (1024 threads, 128 VGPRs) stays free
-// of the walker's register footprint; for unflagged buffers it exits at once.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kSeqThreads = 256;
-
-__global__ __launch_bounds__(kSeqThreads) CDC_WALK_ATTR void k_seq(const Batch B, const DevParams P, const Workspace W)
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
 {
-    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
-    __shared__ uint64_t s_tab[256 * kWCopies];
-#if CDC_RAW_TAB32
-    __shared__ uint64_t s_tab32[256 * 32];
-    __shared__ uint32_t s_tab32_ready;
-    if (threadIdx.x == 0) s_tab32_ready = 0u;
-#define CDC_TAB32_ARGS , s_tab32, &s_tab32_ready
-#else
-#define CDC_TAB32_ARGS
-#endif
-    const uint32_t b = blockIdx.x;
-    if (!B.force_fallback && W.flags[b] == 0) return;
-    fill_gear_lds<kSeqThreads, kWCopies>(s_tab, W.gear);
-    __syncthreads();
-    if (threadIdx.x >= 64) return;
-    const BufDesc &D = B.b[b];
-    const WalkCtx C = make_ctx(B, D, W, reinterpret_cast<const char *>(s_tab) CDC_TAB32_ARGS);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += uint64_t(__shfl_xor((unsigned long long)v, o));
+    return v;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src)
+{
+    return uint64_t(__shfl((unsigned long long)v, int(src)));
+}
+
+// A cut row, stored write-through (two 8-byte relaxed agent stores).
+__device__ __forceinline__ void put_cut(cdc_cut *out, uint64_t off, uint64_t len)
+{
+    uint64_t *w = reinterpret_cast<uint64_t *>(out);
+    st_rlx(w, off);
+    st_rlx(w + 1, len & 0xFFFFFFFFull);
+}
+
+// E (the next segment on the chain, kSegEnd: none) and O (the cuts before it)
+// after segments 0 .. q - 1 of a buffer whose granules start at sg.
+//
+// Segment r's status is a transition of the state E: when E == r (r is on the
+// chain) E becomes conv_r + 1 and its cuts are added; otherwise nothing
+// changes.  The look-back reads the statuses 64 at a time (four windows per
+// round trip), lane j holding segment lo + j, down to the window with the
+// nearest INCLUSIVE status, and composes the transitions of each window: by
+// a prefix sum when every one is trivial (conv_r == r: the chain entered at
+// lo + j runs through the whole window), else by pointer jumping over the
+// lanes (6 rounds of shuffles).  The windows above are kept as one composite
+// F of the first kJ entries of the window above (a chain leaves a window at
+// most kJ segments past its end); a longer jump takes the slow path, q - 1's
+// own INCLUSIVE status.
+constexpr uint32_t kJ = 8;
+constexpr uint32_t kLbWin = 4;  // windows per round trip
+
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v, uint32_t lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = uint64_t(__shfl_up((unsigned long long)v, d));
+        if (lane >= uint32_t(d)) v += t;
+    }
+    return v;
+}
+
+__device__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O)
+{
+    uint32_t Fe = q + lane;  // F, lane t < kJ: entering at hi + 1 + t leaves E = Fe with Fo cuts added
+    uint64_t Fo = 0;
+    bool slow = false;
+    for (int64_t lo0 = int64_t(q) - 64;; lo0 -= 64 * int64_t(kLbWin)) {
+        uint64_t sw[kLbWin];
+#pragma unroll
+        for (uint32_t w = 0; w < kLbWin; ++w) {
+            const int64_t p = lo0 - 64 * int64_t(w) + int64_t(lane);
+            sw[w] = p >= 0 ? ld_rlx(sg + p) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t w = 0; w < kLbWin; ++w) {
+            const int64_t lo = lo0 - 64 * int64_t(w);
+            const int64_t p = lo + int64_t(lane);
+            const bool valid = p >= 0;
+            uint64_t s = sw[w];
+            if (valid) {
+                while (!s) {
+                    __builtin_amdgcn_s_sleep(1);
+                    s = ld_rlx(sg + p);
+                }
+            }
+            const uint64_t im = __ballot(valid && (s >> 62) == 2);
+            const int istar = im ? 63 - int(__builtin_clzll(im)) : -1;  // nearest INCLUSIVE (segment 0 always is)
+            const bool rel = valid && int(lane) > istar;
+            const uint32_t code = uint32_t((s >> 40) & 0x3FFFFFu);
+            const uint64_t cnt = rel ? (s & ((1ull << 40) - 1)) : 0ull;
+            uint32_t ce;
+            uint64_t co;
+            if (!__ballot(rel && code != 0)) {
+                // every transition trivial: entering at lane t runs to the window's end, then through F's entry 0
+                const uint64_t incl = wave_incl_sum64(cnt, lane);
+                const uint64_t tot = readlane64(incl, 63);
+                ce = uint32_t(__builtin_amdgcn_readfirstlane(int(Fe)));
+                co = readlane64(Fo, 0) + tot - (incl - cnt);
+            } else {
+                uint32_t nx = 126;  // next lane on the chain (>= 64: leaves the window; 127: the chain ends)
+                uint64_t add = cnt;
+                if (rel) nx = code == kConvEnd ? 127u : uint32_t(min<uint64_t>(uint64_t(lane) + code + 1, 64 + kJ));
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const uint32_t src = min(nx, 63u);
+                    const uint32_t tn = uint32_t(__shfl(int(nx), int(src)));
+                    const uint64_t ta = shfl64(add, src);
+                    if (nx < 64) {
+                        add += ta;
+                        nx = tn;
+                    }
+                }
+                const uint32_t ft = nx >= 64 && nx < 64 + kJ ? nx - 64 : 0u;
+                const uint32_t fe = uint32_t(__shfl(int(Fe), int(ft)));
+                const uint64_t fo = shfl64(Fo, ft);
+                if (__ballot(rel && nx == 64 + kJ)) slow = true;  // a jump past what F tracks
+                ce = nx == 127 ? kSegEnd : fe;
+                co = add + (nx == 127 ? 0ull : fo);
+            }
+            if (istar >= 0) {
+                const uint64_t si = readlane64(s, istar);
+                const uint32_t ep = uint32_t((si >> 38) & 0xFFFFFFu);
+                const uint64_t op = si & ((1ull << 38) - 1);
+                if (ep == kSegEnd) {
+                    E = kSegEnd;
+                    O = op;
+                    return;
+                }
+                const int64_t t = int64_t(ep) - lo;
+                if (slow || t >= 64 + int64_t(kJ)) goto slow_path;
+                if (t >= 64) {  // passes this window: enters F directly
+                    E = uint32_t(__builtin_amdgcn_readlane(int(Fe), int(t - 64)));
+                    O = op + readlane64(Fo, int(t - 64));
+                } else {
+                    E = uint32_t(__builtin_amdgcn_readlane(int(ce), int(t)));
+                    O = op + readlane64(co, int(t));
+                }
+                return;
+            }
+            Fe = ce;
+            Fo = co;
+        }
+    }
+slow_path:  // q - 1's own INCLUSIVE status
+    uint64_t sq;
+    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) != 2) __builtin_amdgcn_s_sleep(1);
+    E = uint32_t((sq >> 38) & 0xFFFFFFu);
+    O = sq & ((1ull << 38) - 1);
+}
+
+// The sequential walk of a whole buffer (debug mode, lists that overflow):
+// one wave walks next() from offset 0 and writes the cut list and the result row.
+__device__ void resolve_sequential(const WalkCtx &C, const DevParams &P, const BufDesc &D)
+{
     uint64_t p = 0, idx = 0;
     while (p < C.len) {
         const uint64_t nx = next_node(C, P, p);
         if (nx == kUndet) break;
-        if (C.lane == 0 && idx < D.cap) {
-            cdc_cut cut;
-            cut.offset = p;
-            cut.length = uint32_t(nx - p);
-            cut.reserved = 0;
-            D.out[idx] = cut;
-        }
+        if (C.lane == 0 && idx < D.cap) put_cut(D.out + idx, p, nx - p);
         ++idx;
         p = nx;
     }
     if (C.lane == 0) {
-        D.res->ncuts = idx <= D.cap ? idx : D.cap;
-        D.res->consumed = p;
-        D.res->status = idx <= D.cap ? CDC_OK : CDC_E_NOSPACE;
-        D.res->needed = idx;
+        uint64_t *r = reinterpret_cast<uint64_t *>(D.res);
+        st_rlx(&D.res->ncuts, idx <= D.cap ? idx : D.cap);
+        st_rlx(&D.res->consumed, p);
+        st_rlx(r + 2, uint64_t(int64_t(idx <= D.cap ? CDC_OK : CDC_E_NOSPACE)));
+        st_rlx(&D.res->needed, idx);
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_emit: one workgroup per buffer.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum, uint32_t &total)
+__device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams &P, const Workspace &W, uint32_t g,
+                                                const char *tab, GraphLds &L)
 {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(incl, d);
-        if (lane >= uint32_t(d)) incl += t;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (uint32_t w = 0; w < nw; ++w) {
-        const uint32_t x = s_wsum[w];
-        if (w < wave) off += x;
-        tot += x;
-    }
-    __syncthreads();
-    total = tot;
-    return off + incl - v;
-}
-
-constexpr uint32_t kEmitThreads = 512;  // 2 waves per SIMD: fits beside a scan workgroup
-constexpr uint32_t kEmitSlice = 64;     // segments written per emit workgroup
-constexpr uint32_t kEmitMaxWG = 64;     // emit workgroups per buffer
-
-__host__ __device__ inline uint32_t emit_wgs(uint32_t nseg)
-{
-    const uint32_t e = (nseg + kEmitSlice - 1) / kEmitSlice;
-    return e < 1 ? 1 : (e > kEmitMaxWG ? kEmitMaxWG : e);
-}
-
-// grid (kEmitMaxWG-capped workgroups per buffer, nbufs).  Every workgroup of a
-// buffer computes the same selection and prefix offsets (cheap, L2-resident
-// piece records); each then writes the cuts of its own slice of segments,
-// one wave per segment with lane i writing cut i (coalesced).
-__global__ __launch_bounds__(kEmitThreads) void k_emit(const Batch B, const DevParams P, const Workspace W)
-{
-    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
-    // u16 lists (segment indices < kMaxSegs; kConv* sentinels kept in the top
-    // three codes) so that an emit workgroup fits beside a scan workgroup.
-    __shared__ uint16_t s_nt[kNtCap];
-    __shared__ uint16_t s_ntc[kNtCap];  // merge segment of each listed junction
-    __shared__ uint16_t s_ivs[kNtCap], s_ive[kNtCap];
-    __shared__ uint32_t s_off[kEmitSlice * 16];  // output index of the slice's segments (~0: invalid)
-    __shared__ uint32_t s_wsum[16];
-    __shared__ uint32_t s_m, s_niv, s_fail;
-
-    const uint32_t b = blockIdx.y, tid = threadIdx.x;
+    const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
-    const uint32_t NS = D.nseg, G0 = D.seg_base, cap1 = B.cap1, cap2 = B.cap2;
-    const uint32_t nwg = emit_wgs(NS), wg = blockIdx.x;
-    if (wg >= nwg) return;
-    const bool lead = wg == 0 && tid == 0;
-    if (lead && b == 0) dbg_ts(B, kTsEmit);
-    const uint64_t len = D.len;
-    if (lead) W.flags[b] = 0;
-    if (NS == 0) {
-        if (lead) {
-            D.res->ncuts = 0;
-            D.res->consumed = 0;
-            D.res->status = CDC_OK;
-            D.res->needed = 0;
-        }
-        return;
-    }
-    if (B.force_fallback) return;  // k_seq resolves every buffer
-    const uint64_t e0 = W.w1_exit[G0];
-    const bool cont = NS > 1 && e0 != kUndet && e0 < len;
-    // this workgroup's slice of segments
-    const uint32_t per = (NS + nwg - 1) / nwg;
-    const uint32_t qa = wg * per, qb = min(NS, qa + per);
-
-    // Phase 1: compact the junctions that do not simply hand over to the next segment.
-    if (tid == 0) {
-        s_m = 0;
-        s_fail = 0;
-        s_niv = 0;
-    }
-    __syncthreads();
-    if (cont) {
-        for (uint32_t base = 1; base < NS; base += blockDim.x) {
-            const uint32_t q = base + tid;
-            bool nt = false;
-            uint32_t c = 0;
-            if (q < NS) {
-                c = W.piece[G0 + q].conv;
-                nt = c >= kConvOvf || c != q;  // jump = c + 1 differs from q + 1
-            }
-            uint32_t tot;
-            const uint32_t pre = block_excl_scan(nt ? 1u : 0u, s_wsum, tot);
-            const uint32_t m0 = s_m;
-            if (nt && m0 + pre < kNtCap) {
-                s_nt[m0 + pre] = uint16_t(q);
-                s_ntc[m0 + pre] = uint16_t(c >= kConvOvf ? c - 0xFFFF0000u : c);
-            }
-            __syncthreads();
-            if (tid == 0) s_m = m0 + tot;
-            __syncthreads();
-        }
-    }
-    if (lead && b == 0) dbg_ts(B, kTsEmit + 1);
-    // Phase 2: follow the chain from segment 1 over the non-trivial junctions.
-    if (tid == 0 && cont) {
-        const uint32_t m = s_m;
-        uint32_t niv = 0, fail = 0, cur = 1;
-        if (m > kNtCap) {
-            fail = 1;
+    const WalkCtx C = make_ctx(B, D, W, tab);
+    const uint32_t lane = C.lane, base = D.seg_base, q = g - base;
+    const uint64_t seg = B.seg, S0 = uint64_t(q) * seg, segE = S0 + seg, S1 = min(segE, C.len);
+    const bool l0 = lane == 0;
+    if (l0) dbg_ts(B, kTsRes + 8 * g);
+    Graph G;
+    graph_build(C, P, L, G, S0, S1, B, kTsRes + 8 * g);
+    if (l0) dbg_ts(B, kTsRes + 8 * g + 1);
+    bool ovf = false;
+    // ---- A (phase 0) and B (phase 1) share one walk loop: x steps through the
+    // graph where it can (own segment), next_node() elsewhere.
+    uint64_t sv = kUndet, jv = kUndet, cv = kUndet;  // lane i: node i of the speculative chain / junction / merged-into list
+    uint32_t ns = 0, c2 = 0, cns = 0, k = 0, cur = q, conv = kConvEnd, exact = 0;
+    uint64_t X = kUndet, cX = kUndet, ex = kUndet;  // ex: the node after the piece
+    for (uint32_t phase = 0; phase < 2; ++phase) {
+        uint64_t x;
+        if (phase == 0) {
+            x = S0;
         } else {
-            for (uint32_t i = 0; i < m; ++i) {
-                const uint32_t p = s_nt[i];
-                if (p < cur) continue;  // skipped by an earlier junction walk
-                const uint32_t c16 = s_ntc[i];
-                const uint32_t c = c16 >= (kConvOvf & 0xFFFFu) ? c16 + 0xFFFF0000u : c16;
-                if (c == kConvOvf) {
-                    fail = 1;
+            if (q == 0) {  // the true chain starts at 0 = S0: its piece is the speculative chain
+                conv = 0;
+                k = 0;
+                cv = sv;
+                cns = ns;
+                cX = X;
+                ex = X;
+                break;
+            }
+            x = x_dec(wait_granule(W.xg + g - 1));
+            cur = q;
+            cv = sv;
+            cns = ns;
+            cX = X;
+            if (x == kUndet || x >= C.len) {  // the chain ended before this segment
+                ex = x;
+                break;
+            }
+        }
+        uint32_t idx = x < segE ? graph_lookup(G, lane, x) : kGNone;
+        for (;;) {
+            if (phase == 1) {
+                const uint64_t r = x / seg;
+                if (r != cur) {  // entered a later segment: its published speculative chain
+                    const uint64_t xr = wait_granule(W.xg + base + r);
+                    cur = uint32_t(r);
+                    cns = uint32_t((xr >> 56) & 0x7Fu);
+                    cX = x_dec(xr);
+                    cv = lane < cns ? ld_rlx(W.w1_nodes + size_t(base + r) * kMaxList + lane) : kUndet;
+                }
+                const uint64_t m = __ballot(lane < cns && cv == x);
+                if (m) {  // merged into segment cur's speculative chain
+                    k = uint32_t(__ffsll((unsigned long long)m) - 1);
+                    conv = cur;
+                    ex = cX;
                     break;
                 }
-                const uint32_t j = c >= kConvOvf ? NS : c + 1;
-                if (j > p + 1) {
-                    s_ivs[niv] = uint16_t(p + 1);
-                    s_ive[niv] = uint16_t(j);  // j <= NS <= kMaxSegs
-                    ++niv;
-                }
-                cur = j;
-                if (cur >= NS) break;
+            }
+            const uint32_t n = phase == 0 ? ns : c2;
+            if (n >= kMaxList) {  // chains that do not merge: the buffer is resolved sequentially
+                ovf = true;
+                ex = kUndet;
+                break;
+            }
+            if (phase == 0) {
+                if (lane == n) sv = x;
+                ++ns;
+            } else {
+                if (lane == n) jv = x;
+                ++c2;
+            }
+            uint64_t s = kGHard, nx;
+            uint32_t ni = kGNone;
+            if (idx != kGNone) {
+                const int l = int(idx & 63u);
+                s = readlane64(idx < 64u ? G.sp[0] : G.sp[1], l);
+                ni = uint32_t(__builtin_amdgcn_readlane(int(idx < 64u ? G.si[0] : G.si[1]), l));
+            }
+            if (s != kGHard) {
+                nx = s;
+            } else {
+                nx = next_node(C, P, x);
+                ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
+                ++exact;
+            }
+            if (nx == kUndet || nx >= C.len) {  // the chain ends here
+                ex = nx;
+                break;
+            }
+            if (phase == 0 && nx >= segE) {
+                ex = nx;
+                break;
+            }
+            x = nx;
+            idx = nx < segE ? ni : kGNone;
+        }
+        if (phase == 0) {
+            X = ex;
+            if (ovf) ns = 0;
+            if (lane < ns) st_rlx(W.w1_nodes + size_t(g) * kMaxList + lane, sv);
+            drain_stores();
+            if (l0) {
+                st_rlx(W.xg + g, x_enc(X, ns));
+                dbg_ts(B, kTsRes + 8 * g + 2);
             }
         }
-        s_niv = niv;
-        s_fail = fail;
     }
-    __syncthreads();
-    if (s_fail) {
-        if (lead) W.flags[b] = 1;  // k_seq resolves this buffer
-        return;
+    // the piece: nodes jv[0 .. c2) then cv[k .. cns) when merged (conv != kConvEnd); ex follows the last one
+    const uint32_t nodes = c2 + (conv != kConvEnd ? cns - k : 0u);
+    const uint64_t cuts = nodes - ((nodes > 0 && ex == kUndet) ? 1u : 0u);
+    const uint64_t *sgb = W.sg + base;
+    if (ovf && l0) __hip_atomic_store(W.flags + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t E = 0;
+    uint64_t O = 0;
+    if (q > 0) {
+        if (l0) st_rlx(W.sg + g, kKindLocal | (uint64_t(conv == kConvEnd ? kConvEnd : conv - q) << 40) | cuts);
+        lookback(sgb, q, lane, E, O);
     }
-    const uint32_t niv = s_niv;
-    if (lead && b == 0) {
-        dbg_ts(B, kTsEmit + 2);
-        dbg_ts(B, kTsEmit + 8, s_m);
-        dbg_ts(B, kTsEmit + 9, niv);
-    }
-
-    // Phase 3: emitted cuts per valid segment, prefix sum; keep the offsets of this slice.
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < NS; base += blockDim.x) {
-        const uint32_t q = base + tid;
-        bool valid = false;
-        if (q < NS) {
-            if (q == 0) {
-                valid = true;
-            } else if (cont) {
-                int lo = 0, hi = int(niv) - 1, f = -1;  // last interval with start <= q
-                while (lo <= hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (s_ivs[mid] <= q) {
-                        f = mid;
-                        lo = mid + 1;
-                    } else {
-                        hi = mid - 1;
-                    }
-                }
-                valid = !(f >= 0 && q < s_ive[f]);
-            }
-        }
-        uint32_t emit = 0;
-        if (valid) {
-            const Piece pc = W.piece[G0 + q];
-            emit = pc.cnt - ((pc.cnt > 0 && pc.end == kUndet) ? 1u : 0u);
-        }
-        uint32_t tot;
-        const uint32_t pre = block_excl_scan(emit, s_wsum, tot);
-        if (q >= qa && q < qb) s_off[q - qa] = valid ? carry + pre : 0xFFFFFFFFu;
-        carry += tot;
-    }
-    if (lead && b == 0) dbg_ts(B, kTsEmit + 3);
-    __syncthreads();
-
-    // Phase 4: write the slice, one wave per segment, lane i -> cut i of the piece.
-    const uint32_t lane = tid & 63u, wave = tid >> 6, nwave = blockDim.x >> 6;
-    for (uint32_t q = qa + wave; q < qb; q += nwave) {
-        const uint32_t off = s_off[q - qa];
-        if (off == 0xFFFFFFFFu) continue;
-        const Piece pc = W.piece[G0 + q];
-        const uint32_t gs = G0 + (pc.conv < kConvOvf ? pc.conv : 0u);
-        const uint64_t *sn = W.w1_nodes + size_t(gs) * cap1;
-        const uint64_t *list2 = W.w2_nodes + size_t(G0 + q) * cap2;
-        for (uint32_t t0 = 0; t0 < pc.cnt; t0 += 63) {
-            const uint32_t t = t0 + lane;  // lanes 0..62 own nodes, lane 63 only feeds the successor
-            uint64_t v = pc.end;
-            if (t < pc.cnt) v = t < pc.c2 ? list2[t] : sn[pc.k + (t - pc.c2)];
-            const uint64_t succ = __shfl_down(v, 1);
-            if (lane < 63 && t < pc.cnt) {
-                const uint64_t idx = uint64_t(off) + t;
-                if (succ == kUndet) {
-                    D.res->consumed = v;  // the last chunk is not decided yet
+    if (l0) dbg_ts(B, kTsRes + 8 * g + 3);
+    const bool on = E == q;
+    const bool fb = B.force_fallback != 0;
+    if (on && !fb && nodes > 0) {
+        auto node_at = [&](uint32_t u) -> uint64_t {
+            const uint64_t fj = shfl64(jv, min(u, 63u));
+            const uint64_t fc = shfl64(cv, min(u >= c2 ? k + (u - c2) : 0u, 63u));
+            return u >= nodes ? ex : (u < c2 ? fj : fc);
+        };
+        for (uint32_t t0 = 0; t0 < nodes; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            const uint64_t v = node_at(t), s = node_at(t + 1);
+            if (t < nodes) {
+                if (s == kUndet) {
+                    st_rlx(&D.res->consumed, v);  // the last chunk is not decided yet
                 } else {
-                    if (idx < D.cap) {
-                        cdc_cut cut;
-                        cut.offset = v;
-                        cut.length = uint32_t(succ - v);
-                        cut.reserved = 0;
-                        D.out[idx] = cut;
-                    }
-                    if (succ >= len) D.res->consumed = len;
+                    if (O + t < D.cap) put_cut(D.out + O + t, v, s - v);
+                    if (s >= C.len) st_rlx(&D.res->consumed, C.len);
                 }
             }
         }
+        drain_stores();
     }
-    if (lead) {
-        D.res->ncuts = carry <= D.cap ? carry : D.cap;
-        D.res->status = carry <= D.cap ? CDC_OK : CDC_E_NOSPACE;
-        D.res->needed = carry;
-        if (b == 0) dbg_ts(B, kTsEmit + 5);
+    const uint32_t Eq = on ? (conv == kConvEnd ? kSegEnd : conv + 1) : E;
+    const uint64_t Oq = O + (on ? cuts : 0ull);
+    if (l0) {
+        st_rlx(W.sg + g, kKindIncl | (uint64_t(Eq) << 38) | Oq);
+        dbg_ts(B, kTsRes + 8 * g + 4);
+        if (!(B.debug & kDbgGraph)) {
+            dbg_ts(B, kTsRes + 8 * g + 5, G.n);
+            dbg_ts(B, kTsRes + 8 * g + 6, exact);
+            dbg_ts(B, kTsRes + 8 * g + 7, c2);
+        }
     }
+    if (q + 1 != D.nseg) return;
+    // ---- the buffer's last segment: the result row, or the sequential fallback
+    if (fb || __hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        for (uint32_t p = lane; p < q; p += 64)
+            while ((ld_rlx(sgb + p) >> 62) != 2) __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || fb) {
+            resolve_sequential(C, P, D);
+            return;
+        }
+    }
+    if (l0) {
+        uint64_t *r = reinterpret_cast<uint64_t *>(D.res);
+        st_rlx(&D.res->ncuts, Oq <= D.cap ? Oq : D.cap);
+        st_rlx(r + 2, uint64_t(int64_t(Oq <= D.cap ? CDC_OK : CDC_E_NOSPACE)));
+        st_rlx(&D.res->needed, Oq);
+    }
+}
+
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B, const DevParams P, const Workspace W)
+{
+    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __shared__ uint64_t s_tab[256 * kWCopies];
+    __shared__ GraphLds s_graph[kWalkWavesPerWG];
+    __shared__ uint32_t s_ticket;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(W.tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
+    __syncthreads();
+    if (blockIdx.x == 0 && wave == 0) {  // empty buffers have no segment to write their row
+        for (uint32_t i = lane; i < B.nbufs; i += 64) {
+            if (B.b[i].nseg == 0) {
+                B.b[i].res->ncuts = 0;
+                B.b[i].res->consumed = 0;
+                B.b[i].res->status = CDC_OK;
+                B.b[i].res->needed = 0;
+            }
+        }
+    }
+    const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(s_ticket)) * kWalkWavesPerWG + wave;
+    if (g < B.total_segs) resolve_segment(B, P, W, g, reinterpret_cast<const char *>(s_tab), s_graph[wave]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1952,11 +2010,12 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 {
     uint64_t maxlen = 0;
     for (int i = 0; i < nbufs; ++i) maxlen = lens[i] > maxlen ? lens[i] : maxlen;
-    // Resolution segments of 32 Min (2 MiB at the default sizes): fewer,
-    // longer speculative walks occupy fewer CUs beside the next pass's scan
-    // (C1 pipelined: 16 Min 4.47-4.52k GiB/s, 24 4.64k, 32 4.67-4.70k, 48
-    // 4.52k, 64 4.40k; single-pass latency 0.255 -> 0.266 ms).
-    uint64_t mult = 32;
+    // Resolution segments of 16 Min (1 MiB at the default sizes): one k_resolve
+    // wave each.  A segment's successor graph (~32 listed nodes on random data)
+    // is built in one pass of lane-parallel work; 2 MiB segments needed a second
+    // pass in 44 % of the waves (C1 resolution 30 vs 36 us), 512 KiB segments
+    // saved no graph time and doubled the look-back.
+    uint64_t mult = 16;
     if (const char *env = getenv("CDC_SEG_MULT")) {
         const long v = atol(env);
         if (v >= 2 && v <= 1024) mult = uint64_t(v);
@@ -1996,8 +2055,6 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     }
     plan->scan_lane = lane;
     const uint64_t task_bytes = 64ull * lane;
-    plan->cap1 = uint32_t(seg / P.min_size + 3);
-    plan->cap2 = 4 * plan->cap1 + 16;
     uint64_t segs = 0, tasks = 0;
     for (int i = 0; i < nbufs; ++i) {
         segs += (lens[i] + seg - 1) / seg;
@@ -2013,12 +2070,11 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
         return o;
     };
     plan->off_runs = take(tasks * 64 * 8);
-    plan->off_w1_nodes = take(segs * plan->cap1 * 8);
-    plan->off_w1_cnt = take(segs * 4);
-    plan->off_w2_nodes = take(segs * plan->cap2 * 8);
-    plan->off_piece = take(segs * sizeof(Piece));
+    plan->off_w1_nodes = take(segs * 64 * 8);
+    plan->off_xg = take(segs * 8);
+    plan->off_sg = take(segs * 8);
     plan->off_flags = take(kMaxBufsPerLaunch * 4);
-    plan->off_w1_exit = take(segs * 8);
+    plan->off_tick = take(2 * 4);
     plan->off_runsL = take(tasks * 64 * 8);
     plan->off_validL = take(tasks * 4);
     plan->bytes = off;
@@ -2028,7 +2084,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 // Optional live profiling: hipEvents recorded on the launch stream around the
 // scan kernel and around the whole pipeline of each launch group.
 struct ProfRec {
-    hipEvent_t e0, e1, e2;  // before the scan, after the scan, after k_seq
+    hipEvent_t e0, e1, e2;  // before the scan, after the scan, after k_resolve
     uint64_t scan_bytes;
 };
 static std::mutex g_prof_mu;
@@ -2094,18 +2150,11 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     // exit after one look at the MaskS index on ordinary data)
     if (B.total_tasks > 0 && B.maskl_index && !fused)
         hipLaunchKernelGGL(k_scan_l, sgrid, sblock, 0, st, B, P, W);
-    if (B.total_segs > 0 && !B.force_fallback) {
-        const dim3 grid((B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG);
-        hipLaunchKernelGGL(k_walk1, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
-        hipLaunchKernelGGL(k_walk2, grid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
-    }
-    uint32_t maxseg = 0;
-    for (uint32_t i = 0; i < B.nbufs; ++i) maxseg = B.b[i].nseg > maxseg ? B.b[i].nseg : maxseg;
-    hipLaunchKernelGGL(k_emit, dim3(emit_wgs(maxseg), B.nbufs), dim3(kEmitThreads), 0, st, B, P, W);
+    const dim3 rgrid(B.total_segs > 0 ? (B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG : 1u);
     if (prof)
-        hipExtLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, nullptr, pr.e2, 0, B, P, W);
+        hipExtLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, nullptr, pr.e2, 0, B, P, W);
     else
-        hipLaunchKernelGGL(k_seq, dim3(B.nbufs), dim3(kSeqThreads), 0, st, B, P, W);
+        hipLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
     if (prof) {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof_live.push_back(pr);

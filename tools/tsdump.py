@@ -4,8 +4,7 @@
 
 Runs the device path with B.debug & 16, which makes the kernels record
 s_memrealtime (100 MHz) at phase boundaries, then prints where the time of
-the last launch went: scan workgroups, then per-segment walk phases, then
-k_emit phases.  Times are in us, relative to the first scan workgroup start.
+the last launch went: scan workgroups, then the per-segment phases of k_resolve.  Times are in us, relative to the first scan workgroup start.
 """
 import argparse
 import ctypes
@@ -17,11 +16,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-K_SCAN, K_W1 = 0, 4 * 4096
-K_MAXSEGS = 16384
-K_W2 = K_W1 + 8 * K_MAXSEGS
-K_EMIT = K_W2 + 8 * K_MAXSEGS
-K_SLOTS = K_EMIT + 16
+K_SCAN, K_RES = 0, 4 * 4096
+K_SLOTS = K_RES + 8 * 16384
 
 
 def pct(a, qs=(0, 50, 90, 100)):
@@ -55,37 +51,31 @@ def main():
     ts = np.zeros(K_SLOTS, dtype=np.uint64)
     assert L.cdc_debug_timestamps(ts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), K_SLOTS) == 0
     ts = ts.astype(np.int64)
-    scan = ts[K_SCAN:K_W1].reshape(-1, 4)
+    scan = ts[K_SCAN:K_RES].reshape(-1, 4)
     scan = scan[scan[:, 0] > 0]
     t0 = scan[:, 0].min()
     us = lambda x: (x - t0) / 100.0  # 100 MHz
     print(f"scan WGs {len(scan)}: start {pct(us(scan[:, 0]))}")
     print(f"  fill done {pct(us(scan[:, 1]))}")
     print(f"  wave0 end {pct(us(scan[:, 2]))}")
-    idx = np.nonzero(ts[K_SCAN:K_W1].reshape(-1, 4)[:, 0] > 0)[0]
+    idx = np.nonzero(ts[K_SCAN:K_RES].reshape(-1, 4)[:, 0] > 0)[0]
     for x in range(8):  # blockIdx % 8 ~ XCD
         sel = (idx % 8) == x
         print(f"    blk%8={x}: end {pct(us(scan[sel, 2]), (0, 50, 100))}")
-    nseg = int(np.count_nonzero(ts[K_W1:K_W2].reshape(-1, 8)[:, 3]))
-    w1 = ts[K_W1:K_W2].reshape(-1, 8)[:nseg]
-    w2 = ts[K_W2:K_EMIT].reshape(-1, 8)[:nseg]
-    print(f"walk1 segs {nseg}: start {pct(us(w1[:, 0]))}")
-    print(f"  fill done {pct(us(w1[:, 1]))}")
-    print(f"  1st node / preload done {pct(us(w1[:, 2]))}")
-    if w1[:, 5].max() > 0:
-        print(f"  1st spec loop done  {pct(us(w1[:, 7]))}")
-        print(f"  1st spec round done {pct(us(w1[:, 5]))}   rounds {pct(w1[:, 6])}")
-    print(f"  end       {pct(us(w1[:, 3]))}")
-    print(f"  per-wave (end - fill) {pct((w1[:, 3] - w1[:, 1]) / 100.0)}  nodes {pct(w1[:, 4])}")
-    ok = w2[:, 3] > 0
-    print(f"walk2 start {pct(us(w2[:, 0]))}")
-    print(f"  fill done {pct(us(w2[:, 1]))}")
-    print(f"  end       {pct(us(w2[ok, 3]))}")
-    print(f"  per-wave (end - fill) {pct((w2[ok, 3] - w2[ok, 1]) / 100.0)}  steps {pct(w2[ok, 4])}")
-    e = ts[K_EMIT:K_SLOTS]
-    names = ["start", "ph1 done", "ph2 done", "ph3 loads", "ph3 scan", "end"]
-    print("emit " + "  ".join(f"{n}={us(e[i]):.1f}" for i, n in enumerate(names)) +
-          f"  nontrivial={e[8]} intervals={e[9]}")
+    r = ts[K_RES:K_SLOTS].reshape(-1, 8)
+    nseg = int(np.count_nonzero(r[:, 4]))
+    r = r[:nseg]
+    print(f"k_resolve segs {nseg}: start {pct(us(r[:, 0]))}")
+    print(f"  graph built {pct(us(r[:, 1]))}   (built - start) {pct((r[:, 1] - r[:, 0]) / 100.0)}")
+    print(f"  spec exit published {pct(us(r[:, 2]))}   (- built) {pct((r[:, 2] - r[:, 1]) / 100.0)}")
+    lb = r[1:, 3]
+    print(f"  look-back done {pct(us(lb))}   (- spec) {pct((lb - r[1:, 2]) / 100.0)}")
+    print(f"  inclusive published {pct(us(r[:, 4]))}   per wave (end - start) {pct((r[:, 4] - r[:, 0]) / 100.0)}")
+    if os.environ.get("CDC_DEBUG_PHASE") == "48":
+        print(f"  graph: records+list {pct((r[:, 5] - r[:, 0]) / 100.0)}  slot0 {pct((r[:, 6] - r[:, 5]) / 100.0)}"
+              f"  slot1 {pct((r[r[:, 7] > 0, 7] - r[r[:, 7] > 0, 6]) / 100.0)} ({int((r[:, 7] > 0).sum())} segs)")
+        return
+    print(f"  listed nodes {pct(r[:, 5])}   exact next_node() calls {pct(r[:, 6])}   junction nodes {pct(r[:, 7])}")
 
 
 if __name__ == "__main__":
