@@ -88,10 +88,15 @@ typedef struct cdc_result {
  * small/large masks (0 selects the defaults 0x0003590703530000 /
  * 0x0000d90003530000).  cut_convention: 0 = Algorithm returns i (the chunk
  * excludes the byte whose fingerprint matched), 1 = returns i + 1.
- * May be called again to change the parameters; it is not reentrant with
- * in-flight chunking calls. */
+ * May be called again to change the parameters: it waits for the devices to
+ * go idle first, and must not race with other calls.  A different device set
+ * returns CDC_E_INVALID (call cdc_shutdown() first).  A failure leaves the
+ * library uninitialised with nothing allocated. */
 int cdc_init(uint32_t dev_mask, const uint64_t gear[256], uint64_t mask_s, uint64_t mask_l,
              int cut_convention);
+/* 1 while the table in use is the built-in placeholder (cdc_init with gear ==
+ * NULL): cut points then differ from plakar's; pass the real fastcdc.G. */
+int cdc_gear_is_placeholder(void);
 void cdc_shutdown(void);
 const char *cdc_strerror(int status);
 int cdc_abi_version(void);

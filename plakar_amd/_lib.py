@@ -6,6 +6,7 @@ command that builds it.
 """
 import ctypes
 import os
+import warnings
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PLAKAR_CDC_LIB selects an alternative build of the same library (kernel
@@ -101,6 +102,7 @@ SIGNATURES = {
                                                             _P(ctypes.c_void_p), _P(ctypes.c_void_p),
                                                             _P(ctypes.c_void_p), ctypes.c_void_p]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),
@@ -141,6 +143,7 @@ def check(status, what=""):
 
 
 _init_key = None
+_warned_placeholder = False
 
 
 def ensure_init(gear=None, mask_s=0, mask_l=0, cut_convention=0, dev_mask=0):
@@ -163,6 +166,12 @@ def ensure_init(gear=None, mask_s=0, mask_l=0, cut_convention=0, dev_mask=0):
         arr = (ctypes.c_uint64 * 256)(*[int(x) & 0xFFFFFFFFFFFFFFFF for x in gear])
     check(lib().cdc_init(dev_mask, arr, mask_s, mask_l, cut_convention), "cdc_init")
     _init_key = key
+    global _warned_placeholder
+    if gear is None and not _warned_placeholder:
+        _warned_placeholder = True
+        warnings.warn("plakar_amd: the built-in Gear table is a PLACEHOLDER (the go-cdc-chunkers v0.0.8 fastcdc.G "
+                      "is not available here): cut points differ from plakar's; pass the real table as gear=",
+                      stacklevel=2)
 
 
 def default_gear():

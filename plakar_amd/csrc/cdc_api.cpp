@@ -65,7 +65,11 @@ struct DeviceCtx {
 
 struct Global {
     std::mutex mu;
-    bool init = false;
+    // Set (release) once the contexts and the Gear table are in place; entry
+    // points read it (acquire) without the lock.  g.devs changes only inside
+    // cdc_init / cdc_shutdown, which must not race with other calls.
+    std::atomic<bool> init{false};
+    bool placeholder_gear = true;
     uint64_t gear[256];
     uint64_t mask_s = kDefaultMaskS, mask_l = kDefaultMaskL;
     uint32_t cut_adj = 0;
@@ -322,7 +326,7 @@ int group_ws_bytes(const uint64_t *lens, int n, const DevParams &P, uint64_t *by
 int check_ready(int device, DeviceCtx **out)
 {
     Global &g = G();
-    if (!g.init) return CDC_E_NOT_INIT;
+    if (!g.init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
     for (auto *c : g.devs)
         if (c->device == device) {
             *out = c;
@@ -637,73 +641,112 @@ int cdc_device_count(void)
     return n;
 }
 
+static void destroy_ctx(DeviceCtx *c)
+{
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();  // caller streams may still run kernels that write the hint
+    if (c->hint_h) (void)hipHostFree(c->hint_h);
+    if (c->d_gear) (void)hipFree(c->d_gear);
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
+    free_ctx_buffers(c);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
+    delete c;
+}
+
+static int create_ctx(int d, DeviceCtx **out)
+{
+    auto *c = new DeviceCtx();
+    c->device = d;
+    *out = nullptr;
+    if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void **>(&c->d_gear), 256 * sizeof(uint64_t)) != hipSuccess) {
+        destroy_ctx(c);
+        return CDC_E_DEVICE;
+    }
+    if (hipHostMalloc(reinterpret_cast<void **>(&c->hint_h), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
+        hipSuccess) {
+        *c->hint_h = 0u;
+        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->hint_d), c->hint_h, 0) != hipSuccess) {
+            (void)hipHostFree(c->hint_h);
+            c->hint_h = c->hint_d = nullptr;
+        }
+    }
+    *out = c;
+    return CDC_OK;
+}
+
+// Re-initialisation keeps the device set (a different one needs cdc_shutdown
+// first) and waits for every device to go idle before it rewrites the Gear
+// table; cdc_stream objects pick up the new parameters at their next run.  A
+// failure while creating contexts leaves the library uninitialised with
+// nothing allocated.
 int cdc_init(uint32_t dev_mask, const uint64_t gear[256], uint64_t mask_s, uint64_t mask_l,
              int cut_convention)
 {
     Global &g = G();
     std::lock_guard<std::mutex> lock(g.mu);
     if (cut_convention != 0 && cut_convention != 1) return CDC_E_INVALID;
+    uint64_t tab[256];
     if (gear)
-        std::memcpy(g.gear, gear, sizeof(g.gear));
+        std::memcpy(tab, gear, sizeof(tab));
     else
-        cdc_default_gear(g.gear);
-    g.mask_s = mask_s ? mask_s : kDefaultMaskS;
-    g.mask_l = mask_l ? mask_l : kDefaultMaskL;
-    g.cut_adj = uint32_t(cut_convention);
+        cdc_default_gear(tab);
+    const uint64_t ms = mask_s ? mask_s : kDefaultMaskS, ml = mask_l ? mask_l : kDefaultMaskL;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
-        g.init = false;
-        return CDC_E_NO_DEVICE;
-    }
-    if (g.devs.empty()) {
-        for (int d = 0; d < n && d < 32; ++d) {
-            if (dev_mask && !(dev_mask & (1u << d))) continue;
-            auto *c = new DeviceCtx();
-            c->device = d;
-            if (hipSetDevice(d) != hipSuccess) return CDC_E_DEVICE;
-            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-                return CDC_E_DEVICE;
-            if (hipMalloc(reinterpret_cast<void **>(&c->d_gear), 256 * sizeof(uint64_t)) != hipSuccess)
-                return CDC_E_DEVICE;
-            if (hipHostMalloc(reinterpret_cast<void **>(&c->hint_h), 64, hipHostMallocMapped | hipHostMallocCoherent) ==
-                    hipSuccess) {
-                *c->hint_h = 0u;
-                if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->hint_d), c->hint_h, 0) != hipSuccess) {
-                    (void)hipHostFree(c->hint_h);
-                    c->hint_h = c->hint_d = nullptr;
-                }
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return g.devs.empty() ? CDC_E_NO_DEVICE : CDC_E_DEVICE;
+    std::vector<int> want;
+    for (int d = 0; d < n && d < 32; ++d)
+        if (!dev_mask || (dev_mask & (1u << d))) want.push_back(d);
+    if (want.empty()) return CDC_E_NO_DEVICE;
+    if (!g.devs.empty()) {
+        std::vector<int> have;
+        for (auto *c : g.devs) have.push_back(c->device);
+        if (have != want) return CDC_E_INVALID;  // cdc_shutdown() first
+        const bool same = std::memcmp(tab, g.gear, sizeof(tab)) == 0 && ms == g.mask_s && ml == g.mask_l &&
+                          uint32_t(cut_convention) == g.cut_adj;
+        if (same && g.init.load(std::memory_order_acquire)) return CDC_OK;
+        for (auto *c : g.devs)
+            if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return CDC_E_DEVICE;
+    } else {
+        std::vector<DeviceCtx *> made;
+        for (int d : want) {
+            DeviceCtx *c = nullptr;
+            const int st = create_ctx(d, &c);
+            if (st != CDC_OK) {
+                for (auto *m : made) destroy_ctx(m);
+                return st;
             }
-            g.devs.push_back(c);
+            made.push_back(c);
         }
-        if (g.devs.empty()) return CDC_E_NO_DEVICE;
+        g.devs = made;
     }
+    g.init.store(false, std::memory_order_release);
+    std::memcpy(g.gear, tab, sizeof(tab));
+    g.placeholder_gear = gear == nullptr;
+    g.mask_s = ms;
+    g.mask_l = ml;
+    g.cut_adj = uint32_t(cut_convention);
     for (auto *c : g.devs) {
-        if (hipSetDevice(c->device) != hipSuccess) return CDC_E_DEVICE;
-        if (hipMemcpy(c->d_gear, g.gear, sizeof(g.gear), hipMemcpyHostToDevice) != hipSuccess)
+        if (hipSetDevice(c->device) != hipSuccess ||
+            hipMemcpy(c->d_gear, g.gear, sizeof(g.gear), hipMemcpyHostToDevice) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess)
             return CDC_E_DEVICE;
     }
-    g.init = true;
+    g.init.store(true, std::memory_order_release);
     return CDC_OK;
 }
+
+int cdc_gear_is_placeholder(void) { return G().placeholder_gear ? 1 : 0; }
 
 void cdc_shutdown(void)
 {
     Global &g = G();
     std::lock_guard<std::mutex> lock(g.mu);
-    for (auto *c : g.devs) {
-        (void)hipSetDevice(c->device);
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipDeviceSynchronize();  // caller streams may still run kernels that write the hint
-        if (c->hint_h) (void)hipHostFree(c->hint_h);
-        if (c->d_gear) (void)hipFree(c->d_gear);
-        if (c->copy) (void)hipStreamSynchronize(c->copy);
-        free_ctx_buffers(c);
-        if (c->stream) (void)hipStreamDestroy(c->stream);
-        if (c->copy) (void)hipStreamDestroy(c->copy);
-        delete c;
-    }
+    g.init.store(false, std::memory_order_release);
+    for (auto *c : g.devs) destroy_ctx(c);
     g.devs.clear();
-    g.init = false;
 }
 
 int cdc_device_workspace_size(uint64_t len, const cdc_opts *opts, uint64_t *bytes)
@@ -810,7 +853,7 @@ int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out
     const int v = validate_sizes(opts);
     if (v != CDC_OK) return v;
     Global &g = G();
-    if (!g.init) return CDC_E_NOT_INIT;
+    if (!g.init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
     for (int i = 0; i < nbufs; ++i)
         if (bufs[i].len && !bufs[i].data) return CDC_E_INVALID;
     std::vector<HostJob> jobs(nbufs);
@@ -966,6 +1009,20 @@ extern "C" int cdc_stream_commit(cdc_stream *s, uint64_t nbytes, int eof)
 static int stream_run(cdc_stream *s)
 {
     if (hipSetDevice(s->device) != hipSuccess) return CDC_E_DEVICE;
+    // The plan is not monotonic in the length (the scan lane rounds up to
+    // 256 B), so a shorter final fill can need more workspace than the window.
+    s->P = make_params(&s->opts);  // the library's current masks (cdc_init may have changed them)
+    uint64_t need = 0;
+    int wst = cdc_device_workspace_size(s->fill, &s->opts, &need);
+    if (wst != CDC_OK) return wst;
+    if (need > s->ws_bytes) {
+        HIPCHK(hipStreamSynchronize(s->stream));
+        if (s->d_ws) (void)hipFree(s->d_ws);
+        s->d_ws = nullptr;
+        s->ws_bytes = 0;
+        if (hipMalloc(&s->d_ws, need) != hipSuccess) return CDC_E_NOMEM;
+        s->ws_bytes = need;
+    }
     HIPCHK(hipMemcpyAsync(s->d_win, s->h_win, s->fill, hipMemcpyHostToDevice, s->stream));
     const int st = cdc_chunk_device_async(s->device, s->d_win, s->fill, s->eof ? 1 : 0, &s->opts,
                                           s->d_cuts, s->cuts_cap, s->d_res, s->d_ws, s->ws_bytes,
@@ -1027,7 +1084,7 @@ extern "C" int cdc_chunker_new(const char *algorithm, cdc_read_fn read, void *ct
     *out = nullptr;
     cdc_stream *s = nullptr;
     Global &g = G();
-    if (!g.init) return CDC_E_NOT_INIT;
+    if (!g.init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
     const int st = cdc_stream_new(algorithm, opts, 0, g.devs.front()->device, &s);
     if (st != CDC_OK) return st;
     auto *c = new cdc_chunker();

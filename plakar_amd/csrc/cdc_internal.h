@@ -11,16 +11,18 @@ namespace cdc {
 
 constexpr int kMaxBufsPerLaunch = 32;   // buffers per launch group (kernel-arg budget)
 // Candidate index: one u64 record per scan-lane run (scan_lane bytes of one
-// buffer): bits 0-15 the number of full-window MaskS candidates in the run
-// (saturating), bits 16-63 the first kRunCap of them as u16 offsets from the
+// buffer): bits 0-7 the number of full-window MaskS candidates in the run
+// (saturating), bits 8-63 the first kRunCap of them as 14-bit offsets from the
 // run start, ascending.  Written once per run by the lane that scanned it (no
 // atomics, no zeroing); runs and their entries are in position order, so the
 // index is sorted by construction.  A run with more than kRunCap candidates is
-// "dense": walkers rescan its bytes.
-constexpr uint32_t kRunCap = 3;
-constexpr uint32_t kMaxScanLane = 65536;  // run offsets are u16
+// "dense": walkers rescan its bytes (about 0.2 runs per GiB of random data at
+// 0.17 candidates per 5.75-KiB run).
+constexpr uint32_t kRunCap = 4;
+constexpr uint32_t kRecCntBits = 8, kRecEntBits = 14;
+constexpr uint32_t kMaxScanLane = 1u << kRecEntBits;  // run offsets are 14-bit
 constexpr uint32_t kMaxSegs = 1u << 22; // resolution segments per buffer (seg grows past 32 Min beyond)
-constexpr uint32_t kScanLaneBytes = 16384;  // max bytes hashed+tested per scan lane (multiple of 256)
+constexpr uint32_t kScanLaneBytes = 16384;  // max bytes hashed+tested per scan lane (multiple of 256, <= kMaxScanLane)
 #ifndef CDC_WALK_WAVES
 #define CDC_WALK_WAVES 4
 #endif

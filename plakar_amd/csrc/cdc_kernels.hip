@@ -370,6 +370,12 @@ __device__ __forceinline__ uint32_t scan_wave_max(uint32_t v)
     return __builtin_amdgcn_readfirstlane(v);
 }
 
+__device__ __forceinline__ uint32_t rec_cnt(uint64_t rec) { return uint32_t(rec & ((1u << kRecCntBits) - 1)); }
+__device__ __forceinline__ uint32_t rec_ent(uint64_t rec, uint32_t e)
+{
+    return uint32_t(rec >> (kRecCntBits + kRecEntBits * e)) & ((1u << kRecEntBits) - 1);
+}
+
 // Each lane keeps its run's index record in a register (count + the first
 // kRunCap offsets, see cdc_internal.h) and stores it after its last stage:
 // one coalesced 8-byte store per run, no atomics.
@@ -378,9 +384,9 @@ __device__ __forceinline__ void record_hit(uint64_t &rec, int32_t r)
 #if CDC_DIAG_NO_APPEND
     if (r != 0x7FFFFFF0) return;
 #endif
-    const uint32_t c = uint32_t(rec & 0xFFFFu);
-    if (c < kRunCap) rec |= uint64_t(uint32_t(r)) << (16u + 16u * c);
-    if (c < 0xFFFFu) ++rec;
+    const uint32_t c = rec_cnt(rec);
+    if (c < kRunCap) rec |= uint64_t(uint32_t(r)) << (kRecCntBits + kRecEntBits * c);
+    if (c < (1u << kRecCntBits) - 1) ++rec;
 }
 
 // Exact MaskS test of one 16-byte group in the shifted frame, from fp' before
@@ -453,7 +459,7 @@ __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace
         for (int j = 0; j < 4; ++j) {
             const uint64_t r0 = r4 + 64u * j;
             if (r0 > rb) break;
-            const uint64_t E = __ballot((rec[j] & 0xFFFFu) == 0);
+            const uint64_t E = __ballot(rec_cnt(rec[j]) == 0);
             const uint32_t n = uint32_t(min(rb + 1 - r0, uint64_t(64)));
 #if CDC_DIAG_MASKL_TEST == 2
             if (E == 0x123456789ull + n) return true;
@@ -1067,11 +1073,14 @@ __device__ uint64_t raw_scan(const WalkCtx &C, const char *tab, uint32_t laneoff
 {
     const uint64_t H = C.ub + hi, FZ = C.ub + fz;
     uint64_t x = C.ub + lo;
+    // lane slices of up to kRawLaneBytes: a short range (a dense index run) is
+    // spread over every lane, so the serial roll per lane stays short
+    const uint64_t lb = min<uint64_t>(kRawLaneBytes, max<uint64_t>(64, ((hi - lo + 63) / 64 + 15) & ~15ull));
     while (x < H) {
         const uint64_t A = x & ~15ull;
-        const uint64_t bend = min(A + 64ull * kRawLaneBytes, H);
-        const uint64_t ts = max(x, A + uint64_t(C.lane) * kRawLaneBytes);
-        const uint64_t te = min(bend, A + uint64_t(C.lane + 1) * kRawLaneBytes);
+        const uint64_t bend = min(A + 64ull * lb, H);
+        const uint64_t ts = max(x, A + uint64_t(C.lane) * lb);
+        const uint64_t te = min(bend, A + uint64_t(C.lane + 1) * lb);
         uint64_t hit = kNoHit;
         if (ts < te) {
             const uint64_t hs = ts >= FZ + kWarm ? ts - kWarm : FZ;
@@ -1163,11 +1172,11 @@ __device__ __forceinline__ uint64_t run_of(const WalkCtx &C, uint64_t x)
 // >= a is the run's first candidate >= a even when the run is dense.
 __device__ __forceinline__ uint64_t rec_first(uint64_t rec, uint64_t rs, uint64_t a, uint64_t b)
 {
-    const uint32_t n = min(uint32_t(rec & 0xFFFFu), kRunCap);
+    const uint32_t n = min(rec_cnt(rec), kRunCap);
     uint64_t best = kNoHit;
 #pragma unroll
     for (int i = int(kRunCap) - 1; i >= 0; --i) {
-        const uint64_t pos = rs + ((rec >> (16 + 16 * i)) & 0xFFFFu);
+        const uint64_t pos = rs + rec_ent(rec, uint32_t(i));
         if (uint32_t(i) < n && pos >= a && pos < b) best = pos;
     }
     return best;
@@ -1182,7 +1191,7 @@ __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0
     const uint64_t rs = (r0 + C.lane) * C.sl;
     const uint64_t cand = in ? rec_first(rec, rs, a, b) : kNoHit;
     uint64_t mc = __ballot(cand != kNoHit);
-    uint64_t md = __ballot(in && cand == kNoHit && (rec & 0xFFFFu) > kRunCap);
+    uint64_t md = __ballot(in && cand == kNoHit && rec_cnt(rec) > kRunCap);
     done = true;
     while (mc | md) {
         const int lf = mc ? __ffsll((unsigned long long)mc) - 1 : 64;
@@ -1358,7 +1367,10 @@ __device__ __forceinline__ ChunkWin chunk_win(const WalkCtx &C, const DevParams 
 }
 
 // next_node(v) computed by ONE lane from the preloaded records, or kGHard.
-// Identical to next_node() wherever it does not return kGHard.
+// Identical to next_node() wherever it does not return kGHard.  Latency
+// order: the truncated window's 17 dwords are requested first, the record
+// search (LDS only) runs while they are in flight, then the window is rolled
+// with the next 8 Gear gathers always in flight.
 __device__ __forceinline__ uint64_t graph_succ(const WalkCtx &C, const DevParams &P, const GraphLds &L, uint64_t ra,
                                                uint32_t nr, uint64_t v)
 {
@@ -1368,34 +1380,14 @@ __device__ __forceinline__ uint64_t graph_succ(const WalkCtx &C, const DevParams
     const ChunkWin w = chunk_win(C, P, v);
     const uint64_t fz = w.fz, full0 = fz + (P.win - 1);
     if (w.norm_end < full0 || w.lim < full0) return kGHard;  // truncated window not all MaskS / in range
-    // ---- truncated window [fz, full0): fingerprint from 0 at fz, MaskS at every position
     const uint64_t a = C.ub + fz;
     const uint64_t a4 = a & ~3ull, last = (C.ub + E - 1) & ~3ull;  // full0 <= E: the used dwords are in bounds
     const uint32_t sh = uint32_t(a & 3u);
     uint32_t dw[17];
 #pragma unroll
     for (int k = 0; k < 17; ++k) dw[k] = *reinterpret_cast<const uint32_t *>(min<uint64_t>(a4 + 4u * uint64_t(k), last));
-    const uint32_t wm1 = P.win - 1;  // positions tested (<= 63)
-    uint64_t fp = 0;
-    uint32_t first = 63;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t word = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
-        uint64_t gq[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) gq[t] = lds_gear(C.tab, wgear_addr(C.laneoff, word, t));
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const uint32_t j = uint32_t(4 * k + t);
-            if (j >= 63) break;
-            fp = (fp << 1) + gq[t];
-            const bool hit = key_of(fp, P.ms_lo, P.ms_hi) == 0 && j < wm1;
-            first = min(first, hit ? j : 63u);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // 4 gathers in flight at a time: bounded registers
-    }
-    if (first < wm1) return fz + first + P.cut_adj;
-    // ---- full-window MaskS candidates in [full0, s_end) from the records
+    // ---- full-window MaskS candidates in [full0, s_end) from the records (while the bytes load)
+    uint64_t full = kNoHit;  // kGHard: undecided by the records
     const uint64_t s_end = min(w.norm_end, w.lim);
     if (full0 < s_end) {
         const uint64_t rl = run_of(C, s_end - 1);
@@ -1403,7 +1395,10 @@ __device__ __forceinline__ uint64_t graph_succ(const WalkCtx &C, const DevParams
         for (;;) {
             if (r > rl) break;  // no candidate
             uint64_t i = r - ra;
-            if (i >= nr) return kGHard;
+            if (i >= nr) {
+                full = kGHard;
+                break;
+            }
             uint32_t wd = uint32_t(i >> 6);
             uint64_t bits = L.bits[wd] & (~0ull << (i & 63u));
             while (!bits) {
@@ -1412,21 +1407,54 @@ __device__ __forceinline__ uint64_t graph_succ(const WalkCtx &C, const DevParams
                 bits = L.bits[wd];
             }
             if (!bits) {
-                if (ra + nr > rl) break;  // the preload covers the rest: no candidate
-                return kGHard;
+                if (ra + nr <= rl) full = kGHard;  // else: the preload covers the rest, no candidate
+                break;
             }
             i = uint64_t(wd) * 64u + uint64_t(__builtin_ctzll(bits));
             r = ra + i;
             if (r > rl) break;
             const uint64_t rec = L.rec[i];
             const uint64_t cand = rec_first(rec, r * C.sl, full0, s_end);
-            if (cand != kNoHit) return cand + P.cut_adj;
-            if ((rec & 0xFFFFu) > kRunCap) return kGHard;  // dense: the stored entries do not answer
+            if (cand != kNoHit) {
+                full = cand + P.cut_adj;
+                break;
+            }
+            if (rec_cnt(rec) > kRunCap) {  // dense: the stored entries do not answer
+                full = kGHard;
+                break;
+            }
             ++r;
         }
     }
-    if (max(w.norm_end, full0) < w.lim) return kGHard;  // MaskL region: index or raw scan
-    return w.lim;                                        // forced cut at v + n
+    if (full == kNoHit) full = max(w.norm_end, full0) < w.lim ? kGHard : w.lim;  // MaskL region / forced cut
+    // ---- truncated window [fz, full0): fingerprint from 0 at fz, MaskS at every position; it decides first
+    const uint32_t wm1 = P.win - 1;  // positions tested (<= 63)
+    uint64_t fp = 0;
+    uint32_t first = 63;
+    uint32_t wd2[16];  // bytes fz + 4 k .. fz + 4 k + 3
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wd2[k] = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+    uint64_t gq[2][8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) gq[0][t] = lds_gear(C.tab, wgear_addr(C.laneoff, wd2[t >> 2], t & 3));
+#pragma unroll
+    for (int grp = 0; grp < 8; ++grp) {
+        if (grp + 1 < 8) {  // the next 8 gathers in flight while this group rolls
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                gq[(grp + 1) & 1][t] = lds_gear(C.tab, wgear_addr(C.laneoff, wd2[2 * (grp + 1) + (t >> 2)], t & 3));
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t j = uint32_t(8 * grp + t);
+            if (j >= 63) break;
+            fp = (fp << 1) + gq[grp & 1][t];
+            const bool hit = key_of(fp, P.ms_lo, P.ms_hi) == 0 && j < wm1;
+            first = min(first, hit ? j : 63u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return first < wm1 ? fz + first + P.cut_adj : full;
 }
 
 // The segment's listed nodes and their successors, held two per lane.
@@ -1448,6 +1476,22 @@ __device__ __forceinline__ uint32_t graph_find(const GraphLds &L, uint32_t n, ui
     return lo < n && L.node[lo] == x ? lo : kGNone;
 }
 
+// Lane r: the index of the r-th set bit of m (any value when r >= popcount(m)).
+__device__ __forceinline__ uint32_t mask_rank_pos(uint64_t m, uint32_t r)
+{
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 32; w; w >>= 1) {
+        const uint32_t c = uint32_t(__popcll(m & ((1ull << w) - 1)));
+        if (r >= c) {
+            r -= c;
+            m >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
 // Wave-uniform list index of node x, or kGNone.
 __device__ __forceinline__ uint32_t graph_lookup(const Graph &G, uint32_t lane, uint64_t x)
 {
@@ -1465,8 +1509,8 @@ __device__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, G
     const bool tg = (B.debug & kDbgGraph) && C.lane == 0;
     const uint32_t lane = C.lane;
     const uint64_t adj = P.cut_adj;
-    const uint64_t clo = S0 >= adj ? S0 - adj : 0, chi = S1 - adj;  // candidates c with c + adj in [S0, S1)
-    const uint64_t ra = run_of(C, clo);
+    const uint64_t clo = S0 + 1 - adj, chi = S1 - adj;  // candidates c with c + adj in (S0, S1); S0 is node 0
+    const uint64_t ra = run_of(C, S0 >= adj ? S0 - adj : 0);  // <= run_of(clo), <= rneed
     const uint64_t rneed = run_of(C, min(C.len, S1 + P.normal_size) - 1);
     const uint32_t nr = uint32_t(min<uint64_t>(rneed - ra + 1, kGRecs));
     uint64_t recs[kGRecs / 64];
@@ -1475,7 +1519,8 @@ __device__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, G
         const uint32_t i = 64u * k + lane;
         recs[k] = 64u * k < nr && i < nr ? C.runs[ra + i] : 0ull;
     }
-    uint32_t n = 0;
+    uint32_t n = 1;  // node 0: the segment start (the speculative chain's first node)
+    if (lane == 0) L.node[0] = S0;
     const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
     for (uint32_t k = 0; k < kGRecs / 64; ++k) {
@@ -1483,29 +1528,29 @@ __device__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, G
         const uint32_t i = 64u * k + lane;
         const uint64_t rec = recs[k];
         if (i < nr) L.rec[i] = rec;
-        const uint64_t nb = __ballot(i < nr && (rec & 0xFFFFu) != 0);
+        const uint64_t nb = __ballot(i < nr && rec_cnt(rec) != 0);
         if (lane == 0) L.bits[k] = nb;
         // stored entries with c in [clo, chi): a contiguous range of the (ascending) entries
         const uint64_t rs = (ra + i) * C.sl;
-        const uint32_t cnt = i < nr ? min(uint32_t(rec & 0xFFFFu), kRunCap) : 0u;
-        uint32_t e0 = 3, e1 = 0;  // listed entries [e0, e1)
+        const uint32_t cnt = i < nr ? min(rec_cnt(rec), kRunCap) : 0u;
+        uint32_t e0 = kRunCap, e1 = 0;  // listed entries [e0, e1)
 #pragma unroll
         for (uint32_t e = 0; e < kRunCap; ++e) {
-            const uint64_t c = rs + ((rec >> (16 + 16 * e)) & 0xFFFFu);
+            const uint64_t c = rs + rec_ent(rec, e);
             if (e < cnt && c >= clo && c < chi) {
                 e0 = min(e0, e);
                 e1 = e + 1;
             }
         }
         const uint32_t kk = e1 > e0 ? e1 - e0 : 0u;
-        const uint64_t b0 = __ballot(kk & 1u), b1 = __ballot(kk & 2u);
-        const uint32_t pre = uint32_t(__popcll(b0 & below) + 2 * __popcll(b1 & below));
+        const uint64_t b0 = __ballot(kk & 1u), b1 = __ballot(kk & 2u), b2 = __ballot(kk & 4u);
+        const uint32_t pre = uint32_t(__popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below));
 #pragma unroll
         for (uint32_t e = 0; e < kRunCap; ++e) {
             const uint32_t o = n + pre + (e - e0);
-            if (e >= e0 && e < e1 && o < kGNodes) L.node[o] = rs + ((rec >> (16 + 16 * e)) & 0xFFFFu) + adj;
+            if (e >= e0 && e < e1 && o < kGNodes) L.node[o] = rs + rec_ent(rec, e) + adj;
         }
-        n += uint32_t(__popcll(b0) + 2 * __popcll(b1));
+        n += uint32_t(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
     }
     for (uint32_t k = (nr + 63) / 64; k < kGRecs / 64; ++k)
         if (lane == 0) L.bits[k] = 0;
@@ -1608,7 +1653,8 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
 // are zeroed by the scan kernel of the same launch group.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMaxList = 64;                // nodes per register list
-constexpr uint64_t kX56 = (1ull << 56) - 1;      // xg: X in bits 0-55 (all ones: kUndet)
+constexpr uint64_t kX55 = (1ull << 55) - 1;      // xg: X in bits 0-54 (all ones: kUndet), node count 55-61,
+constexpr uint64_t kXNodes = 1ull << 62;         //     62: the node list is readable, 63: X is published
 constexpr uint64_t kKindLocal = 1ull << 62, kKindIncl = 2ull << 62;
 constexpr uint32_t kConvEnd = 0x3FFFFFu;         // LOCAL: the chain ends in this piece (or before it)
 constexpr uint32_t kSegEnd = 0xFFFFFFu;          // INCLUSIVE: no further segment on the chain
@@ -1638,10 +1684,10 @@ __device__ __forceinline__ uint64_t wait_granule(const uint64_t *p)
     }
 }
 
-__device__ __forceinline__ uint64_t x_dec(uint64_t g) { return (g & kX56) == kX56 ? kUndet : (g & kX56); }
+__device__ __forceinline__ uint64_t x_dec(uint64_t g) { return (g & kX55) == kX55 ? kUndet : (g & kX55); }
 __device__ __forceinline__ uint64_t x_enc(uint64_t x, uint32_t ns)
 {
-    return (1ull << 63) | (uint64_t(ns) << 56) | (x == kUndet || x >= kX56 ? kX56 : x);
+    return (1ull << 63) | (uint64_t(ns) << 55) | (x == kUndet || x >= kX55 ? kX55 : x);
 }
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
@@ -1678,17 +1724,28 @@ __device__ __forceinline__ void put_cut(cdc_cut *out, uint64_t off, uint64_t len
 // F of the first kJ entries of the window above (a chain leaves a window at
 // most kJ segments past its end); a longer jump takes the slow path, q - 1's
 // own INCLUSIVE status.
+// k_resolve register budget: at most 128 VGPRs lets a resolve workgroup sit
+// beside a scan workgroup (3 waves x 128 per SIMD) on every CU, so a batch's
+// resolution never holds CUs the next batch's scan is waiting for.
+#ifndef CDC_RESOLVE_WPE
+#define CDC_RESOLVE_WPE 0
+#endif
+#if CDC_RESOLVE_WPE
+#define CDC_RESOLVE_ATTR __attribute__((amdgpu_waves_per_eu(CDC_RESOLVE_WPE)))
+#else
+#define CDC_RESOLVE_ATTR
+#endif
 constexpr uint32_t kJ = 8;
-constexpr uint32_t kLbWin = 4;  // windows per round trip
+constexpr uint32_t kLbWin = 8;  // windows per round trip
 
-__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v, uint32_t lane)
+// Inclusive prefix sum within each 16-lane row (DPP, no LDS round trip).
+__device__ __forceinline__ uint32_t row_incl_sum32(uint32_t x)
 {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = uint64_t(__shfl_up((unsigned long long)v, d));
-        if (lane >= uint32_t(d)) v += t;
-    }
-    return v;
+    x += __builtin_amdgcn_update_dpp(0u, x, kDppRowShr + 1, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0u, x, kDppRowShr + 2, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0u, x, kDppRowShr + 4, 0xF, 0xF, true);
+    x += __builtin_amdgcn_update_dpp(0u, x, kDppRowShr + 8, 0xF, 0xF, true);
+    return x;
 }
 
 __device__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O)
@@ -1723,11 +1780,21 @@ __device__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t
             uint32_t ce;
             uint64_t co;
             if (!__ballot(rel && code != 0)) {
-                // every transition trivial: entering at lane t runs to the window's end, then through F's entry 0
-                const uint64_t incl = wave_incl_sum64(cnt, lane);
-                const uint64_t tot = readlane64(incl, 63);
+                // every transition trivial: entering at lane t runs to the window's end, then through
+                // F's entry 0.  Counts per segment fit 32 bits; only the lanes below kJ (row 0) and
+                // entries above the INCLUSIVE one (any row) are used, so row prefixes plus the row
+                // totals give each lane's suffix.
+                const uint32_t c32 = uint32_t(cnt);
+                const uint32_t incl = row_incl_sum32(c32);
+                const uint32_t r0 = uint32_t(__builtin_amdgcn_readlane(int(incl), 15));
+                const uint32_t r1 = uint32_t(__builtin_amdgcn_readlane(int(incl), 31));
+                const uint32_t r2 = uint32_t(__builtin_amdgcn_readlane(int(incl), 47));
+                const uint32_t r3 = uint32_t(__builtin_amdgcn_readlane(int(incl), 63));
+                const uint32_t row = lane >> 4;
+                const uint32_t before = (row > 0 ? r0 : 0u) + (row > 1 ? r1 : 0u) + (row > 2 ? r2 : 0u);
+                const uint64_t tot = uint64_t(r0) + r1 + r2 + r3;
                 ce = uint32_t(__builtin_amdgcn_readfirstlane(int(Fe)));
-                co = readlane64(Fo, 0) + tot - (incl - cnt);
+                co = readlane64(Fo, 0) + tot - uint64_t(before + incl - c32);
             } else {
                 uint32_t nx = 126;  // next lane on the chain (>= 64: leaves the window; 127: the chain ends)
                 uint64_t add = cnt;
@@ -1815,15 +1882,42 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     graph_build(C, P, L, G, S0, S1, B, kTsRes + 8 * g);
     if (l0) dbg_ts(B, kTsRes + 8 * g + 1);
     bool ovf = false;
-    // ---- A (phase 0) and B (phase 1) share one walk loop: x steps through the
-    // graph where it can (own segment), next_node() elsewhere.
+    // ---- A (phase 0) and B (phase 1).  While the walk stays on listed nodes
+    // of a graph that fits one register (n <= 64: every 1-MiB segment of
+    // random data), it is a scalar loop over node indices collecting a bit
+    // mask; the node list is then built lane-parallel.  Anything else (a
+    // kGHard node, an unlisted successor, another segment) goes through the
+    // general loop: the graph where it answers, next_node() elsewhere.
+    const bool g64 = G.n <= 64;
     uint64_t sv = kUndet, jv = kUndet, cv = kUndet;  // lane i: node i of the speculative chain / junction / merged-into list
     uint32_t ns = 0, c2 = 0, cns = 0, k = 0, cur = q, conv = kConvEnd, exact = 0;
     uint64_t X = kUndet, cX = kUndet, ex = kUndet;  // ex: the node after the piece
+    uint64_t pm = 0;                                 // graph nodes on the speculative chain (g64)
     for (uint32_t phase = 0; phase < 2; ++phase) {
         uint64_t x;
+        bool rec = true;  // false: x is recorded already, step from it
+        bool done = false;
         if (phase == 0) {
             x = S0;
+            if (g64) {  // node 0 is S0
+                uint32_t gi = 0;
+                for (;;) {
+                    pm |= 1ull << gi;
+                    const uint32_t nxt = uint32_t(__builtin_amdgcn_readlane(int(G.si[0]), int(gi)));
+                    if (nxt == kGNone) break;
+                    gi = nxt;
+                }
+                ns = uint32_t(__popcll(pm));
+                sv = shfl64(G.v[0], mask_rank_pos(pm, lane));
+                if (lane >= ns) sv = kUndet;
+                const uint64_t sz = readlane64(G.sp[0], int(gi));
+                if (sz == kGHard) {
+                    x = readlane64(G.v[0], int(gi));
+                    rec = false;
+                } else {
+                    x = sz;
+                }
+            }
         } else {
             if (q == 0) {  // the true chain starts at 0 = S0: its piece is the speculative chain
                 conv = 0;
@@ -1834,81 +1928,127 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 ex = X;
                 break;
             }
-            x = x_dec(wait_granule(W.xg + g - 1));
+            const uint64_t xp = wait_granule(W.xg + g - 1);  // its load drained this wave's node-list stores
+            drain_stores();
+            if (l0) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
+            x = x_dec(xp);
             cur = q;
             cv = sv;
             cns = ns;
             cX = X;
-            if (x == kUndet || x >= C.len) {  // the chain ended before this segment
-                ex = x;
-                break;
+            if (g64 && x >= S0 && x < segE) {
+                const uint32_t ia = graph_lookup(G, lane, x);
+                if (ia != kGNone) {
+                    uint64_t pj = 0;
+                    uint32_t gi = ia;
+                    bool merged = false;
+                    for (;;) {
+                        if ((pm >> gi) & 1ull) {
+                            merged = true;
+                            break;
+                        }
+                        pj |= 1ull << gi;
+                        const uint32_t nxt = uint32_t(__builtin_amdgcn_readlane(int(G.si[0]), int(gi)));
+                        if (nxt == kGNone) break;
+                        gi = nxt;
+                    }
+                    c2 = uint32_t(__popcll(pj));
+                    jv = shfl64(G.v[0], mask_rank_pos(pj, lane));
+                    if (lane >= c2) jv = kUndet;
+                    const uint64_t vg = readlane64(G.v[0], int(gi));
+                    if (merged) {
+                        const uint64_t m = __ballot(lane < ns && sv == vg);
+                        k = uint32_t(__ffsll((unsigned long long)m) - 1);
+                        conv = q;
+                        ex = X;
+                        done = true;
+                    } else {
+                        const uint64_t sz = readlane64(G.sp[0], int(gi));
+                        if (sz == kGHard) {
+                            x = vg;
+                            rec = false;
+                        } else {
+                            x = sz;
+                        }
+                    }
+                }
             }
         }
-        uint32_t idx = x < segE ? graph_lookup(G, lane, x) : kGNone;
-        for (;;) {
-            if (phase == 1) {
-                const uint64_t r = x / seg;
-                if (r != cur) {  // entered a later segment: its published speculative chain
-                    const uint64_t xr = wait_granule(W.xg + base + r);
-                    cur = uint32_t(r);
-                    cns = uint32_t((xr >> 56) & 0x7Fu);
-                    cX = x_dec(xr);
-                    cv = lane < cns ? ld_rlx(W.w1_nodes + size_t(base + r) * kMaxList + lane) : kUndet;
+        uint32_t idx = kGNone;
+        if (!done) {
+            if (rec && x < segE) idx = graph_lookup(G, lane, x);
+            for (;;) {
+                if (rec) {
+                    if (x == kUndet || x >= C.len || (phase == 0 && x >= segE)) {  // the chain ends / leaves
+                        ex = x;
+                        break;
+                    }
+                    if (phase == 1) {
+                        const uint64_t r = x / seg;
+                        if (r != cur) {  // entered a later segment: its published speculative chain
+                            uint64_t xr;
+                            while (!((xr = readlane64(ld_rlx(W.xg + base + r), 0)) & kXNodes))
+                                __builtin_amdgcn_s_sleep(1);
+                            cur = uint32_t(r);
+                            cns = uint32_t((xr >> 55) & 0x7Fu);
+                            cX = x_dec(xr);
+                            cv = lane < cns ? ld_rlx(W.w1_nodes + size_t(base + r) * kMaxList + lane) : kUndet;
+                        }
+                        const uint64_t m = __ballot(lane < cns && cv == x);
+                        if (m) {  // merged into segment cur's speculative chain
+                            k = uint32_t(__ffsll((unsigned long long)m) - 1);
+                            conv = cur;
+                            ex = cX;
+                            break;
+                        }
+                    }
+                    const uint32_t n = phase == 0 ? ns : c2;
+                    if (n >= kMaxList) {  // chains that do not merge: the buffer is resolved sequentially
+                        ovf = true;
+                        ex = kUndet;
+                        break;
+                    }
+                    if (phase == 0) {
+                        if (lane == n) sv = x;
+                        ++ns;
+                        if (g64 && idx != kGNone) pm |= 1ull << idx;
+                    } else {
+                        if (lane == n) jv = x;
+                        ++c2;
+                    }
                 }
-                const uint64_t m = __ballot(lane < cns && cv == x);
-                if (m) {  // merged into segment cur's speculative chain
-                    k = uint32_t(__ffsll((unsigned long long)m) - 1);
-                    conv = cur;
-                    ex = cX;
-                    break;
+                rec = true;
+                uint64_t s = kGHard, nx;
+                uint32_t ni = kGNone;
+                if (idx != kGNone) {
+                    const int l = int(idx & 63u);
+                    s = readlane64(idx < 64u ? G.sp[0] : G.sp[1], l);
+                    ni = uint32_t(__builtin_amdgcn_readlane(int(idx < 64u ? G.si[0] : G.si[1]), l));
                 }
+                if (s != kGHard) {
+                    nx = s;
+                } else {
+                    nx = next_node(C, P, x);
+                    ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
+                    ++exact;
+                }
+                x = nx;
+                idx = nx < segE ? ni : kGNone;
             }
-            const uint32_t n = phase == 0 ? ns : c2;
-            if (n >= kMaxList) {  // chains that do not merge: the buffer is resolved sequentially
-                ovf = true;
-                ex = kUndet;
-                break;
-            }
-            if (phase == 0) {
-                if (lane == n) sv = x;
-                ++ns;
-            } else {
-                if (lane == n) jv = x;
-                ++c2;
-            }
-            uint64_t s = kGHard, nx;
-            uint32_t ni = kGNone;
-            if (idx != kGNone) {
-                const int l = int(idx & 63u);
-                s = readlane64(idx < 64u ? G.sp[0] : G.sp[1], l);
-                ni = uint32_t(__builtin_amdgcn_readlane(int(idx < 64u ? G.si[0] : G.si[1]), l));
-            }
-            if (s != kGHard) {
-                nx = s;
-            } else {
-                nx = next_node(C, P, x);
-                ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
-                ++exact;
-            }
-            if (nx == kUndet || nx >= C.len) {  // the chain ends here
-                ex = nx;
-                break;
-            }
-            if (phase == 0 && nx >= segE) {
-                ex = nx;
-                break;
-            }
-            x = nx;
-            idx = nx < segE ? ni : kGNone;
         }
         if (phase == 0) {
             X = ex;
             if (ovf) ns = 0;
+            // X at once; the node list (read only by junctions that cross into this
+            // segment) is flagged readable once a later load has drained its stores
             if (lane < ns) st_rlx(W.w1_nodes + size_t(g) * kMaxList + lane, sv);
-            drain_stores();
             if (l0) {
                 st_rlx(W.xg + g, x_enc(X, ns));
                 dbg_ts(B, kTsRes + 8 * g + 2);
+            }
+            if (q == 0) {
+                drain_stores();
+                if (l0) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
             }
         }
     }
@@ -1975,7 +2115,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     }
 }
 
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B, const DevParams P, const Workspace W)
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_RESOLVE_ATTR void k_resolve(const Batch B, const DevParams P, const Workspace W)
 {
     __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];

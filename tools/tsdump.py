@@ -75,6 +75,11 @@ def main():
         print(f"  graph: records+list {pct((r[:, 5] - r[:, 0]) / 100.0)}  slot0 {pct((r[:, 6] - r[:, 5]) / 100.0)}"
               f"  slot1 {pct((r[r[:, 7] > 0, 7] - r[r[:, 7] > 0, 6]) / 100.0)} ({int((r[:, 7] > 0).sum())} segs)")
         return
+    slow = np.argsort(r[:, 2] - r[:, 0])[-4:]
+    print("  slowest speculative chains (segment: us, exact calls, listed): " +
+          ", ".join(f"{i}: {(r[i, 2] - r[i, 0]) / 100.0:.1f}, {r[i, 6]}, {r[i, 5]}" for i in slow))
+    lbs = np.argsort(r[:, 3])[-4:]
+    print("  latest look-backs (segment: done at us): " + ", ".join(f"{i}: {us(r[i, 3]):.1f}" for i in lbs))
     print(f"  listed nodes {pct(r[:, 5])}   exact next_node() calls {pct(r[:, 6])}   junction nodes {pct(r[:, 7])}")
 
 
