@@ -37,10 +37,7 @@
 namespace cdc {
 
 static constexpr uint64_t kNoHit = ~0ull;
-#ifndef CDC_RAW_LANE
-#define CDC_RAW_LANE 512
-#endif
-static constexpr uint32_t kRawLaneBytes = CDC_RAW_LANE;  // bytes tested per lane per raw-scan block
+static constexpr uint32_t kRawLaneBytes = 512;  // bytes tested per lane per raw-scan block (C3 +5-8 % over 256)
 static constexpr uint32_t kWarm = 64;           // warm-up bytes (>= W - 1 for any mask)
 
 // ---------------------------------------------------------------------------
@@ -73,24 +70,10 @@ __device__ __forceinline__ void fill_gear_lds(uint64_t *tab, const uint64_t *gea
         if (x < kSlots) tab[x] = v[i] << sh;
     }
 }
-// Walker register cap: the scan holds 3 waves x 112 VGPRs per SIMD, so a
-// walker wave fits beside it (and one batch's resolution runs beside the next
-// batch's scan) only at <= 176 VGPRs (512 - 336).
-#ifndef CDC_WALK_WPE
-#define CDC_WALK_WPE 0
-#endif
-#if CDC_WALK_WPE
-#define CDC_WALK_ATTR __attribute__((amdgpu_waves_per_eu(CDC_WALK_WPE)))
-#else
-#define CDC_WALK_ATTR
-#endif
 // Walker table copies: 8 by default (16 KiB).  32 (the scan's layout:
 // conflict-free gathers, one-instruction v_perm address) made C3's raw MaskL
 // scans 3.5 % faster but C1 2 % slower (a 64-KiB fill per walker workgroup).
-#ifndef CDC_WALK_COPIES
-#define CDC_WALK_COPIES 8
-#endif
-constexpr uint32_t kWCopies = CDC_WALK_COPIES;
+constexpr uint32_t kWCopies = 8;
 constexpr uint32_t kWEntShift = kWCopies == 32 ? 8 : kWCopies == 16 ? 7 : 6;  // log2(kWCopies * 8)
 static_assert(kWCopies == 8 || kWCopies == 16 || kWCopies == 32, "walker table copies");
 
@@ -132,27 +115,12 @@ __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
 }
 
 // Roll 16 bytes and return the min of the 16 keys (0 iff some position hit).
-// CDC_ROLL_MIN3=1 reduces the keys with v_min3 after the roll instead (C3 5 %
-// slower: the keys stay live across the chain).
-#ifndef CDC_ROLL_MIN3
-#define CDC_ROLL_MIN3 0
-#endif
+// (Reducing the keys with v_min3 after the roll instead was 5 % slower on C3:
+// the keys stay live across the chain.)
 template <uint32_t ESH = kWEntShift>
 __device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, const char *tab,
                                                 uint32_t laneoff, uint32_t mlo, uint32_t mhi)
 {
-#if CDC_ROLL_MIN3
-    uint32_t key[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        fp = (fp << 1) + lds_gear(tab, wgear_addr<ESH>(laneoff, word_of(d, k >> 2), k));
-        key[k] = key_of(fp, mlo, mhi);
-    }
-    uint32_t acc = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) acc = umin3(acc, key[k], key[k + 1]);
-    return acc;
-#else
     uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -160,7 +128,6 @@ __device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, co
         acc = min(acc, key_of(fp, mlo, mhi));
     }
     return acc;
-#endif
 }
 
 template <uint32_t ESH = kWEntShift>
@@ -220,12 +187,10 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: the byte scan.  Each wave owns 64 lane runs of B.scan_lane bytes;
-// per stage of kStage bytes per lane it issues kL global_load_lds_dwordx4
-// (1 KiB each; every 64-B line half read whole by adjacent lanes) into a
-// private kNBuf-deep LDS ring, and each lane reads its own kStage bytes back
-// with ds_read_b128 through an XOR swizzle (piece p of lane c at slot
-// p ^ stage_swz(c)) that makes the reads bank-conflict-free.
+// k_scan: the byte scan.  Each wave owns 64 lane runs of B.scan_lane bytes
+// and stages them through one 4-KiB LDS slot per wave with LDS-DMA
+// (global_load_lds_dwordx4, 4 per stage of 64 B per lane): pair staging,
+// described at scan_body.
 //
 // The fingerprint runs in a shifted frame: the LDS Gear table holds
 // G[b] << sh with sh = 63 - (highest MaskS bit), so fp' = fp << sh keeps every
@@ -238,51 +203,23 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 // the lane's run and lanes past the buffer's end need no separate code path:
 // every stage of every lane runs the same straight-line loop.
 //
-// Software pipeline, per wave: the DMA of stage t + kNBuf - 1 is issued at the
-// top of stage t into the slot stage t - 1 vacated; the next stage's data is
-// read (ds_read_b128) at the start of the current stage's last group, and the
-// next group's 16 Gear gathers are issued a quarter at a time into the
+// The next group's 16 Gear gathers are issued a quarter at a time into the
 // registers the current group's roll has just consumed.
 //
 // DMA addressing: one wave-uniform 64-bit base (SGPR pair) and one 32-bit
-// per-lane offset per piece, advanced by kStage per stage and clamped to the
-// buffer's last 16-byte block (v_add + v_min per piece), so the warm-up before
-// byte 0 and the ragged end read in-bounds bytes that the exact recheck then
-// ignores.
+// per-lane offset per piece, the base advanced per stage; a wave whose pieces
+// could leave the buffer clamps them to the buffer's last 16-byte block, so
+// the warm-up before byte 0 and the ragged end read in-bounds bytes that the
+// exact recheck then ignores.
 // ---------------------------------------------------------------------------
-#ifndef CDC_SCAN_WAVES
-#define CDC_SCAN_WAVES 12
-#endif
-#ifndef CDC_SCAN_NBUF
-#define CDC_SCAN_NBUF 1
-#endif
-#ifndef CDC_SCAN_STAGE
-#define CDC_SCAN_STAGE 64
-#endif
-#ifndef CDC_SCAN_PAIRS
-#define CDC_SCAN_PAIRS 1
-#endif
-#ifndef CDC_EARLY_ISSUE
-#define CDC_EARLY_ISSUE 1
-#endif
-#ifndef CDC_SCAN_V2
-#define CDC_SCAN_V2 1
-#endif
-#ifndef CDC_TAIL_PRIO
-#define CDC_TAIL_PRIO 3
-#endif
 
-constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
-constexpr uint32_t kStage = CDC_SCAN_STAGE;           // bytes per lane per stage (32 or 64)
+constexpr uint32_t kS2Waves = 12;                     // waves per scan workgroup (one workgroup per CU)
+constexpr uint32_t kStage = 64;                       // bytes per lane per stage
 constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane per stage = DMAs per stage
 constexpr uint32_t kGroups = kStage / 16;             // 16-byte groups per stage
-static_assert(kStage == 32 || kStage == 64 || kStage == 128, "stage size");
-constexpr uint32_t kNBuf = CDC_SCAN_NBUF;             // ring depth (kNBuf - 1 stages in flight)
-[[maybe_unused]] constexpr uint32_t kAhead = kNBuf - 1;
-constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage
+constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage (one LDS slot)
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
-static_assert(kNBuf >= 1 && kNBuf <= 3, "ring depth");
-static_assert(kGearLdsBytes + kS2Waves * kNBuf * kStageBytes <= 160u * 1024u, "LDS budget");
+static_assert(kGearLdsBytes + kS2Waves * kStageBytes <= 160u * 1024u, "LDS budget");
 // Scan lane lengths are multiples of kLaneQuant (16-B aligned runs: every lane
 // of a buffer has the same stage alignment; 256 B avoided the slow strides
 // seen at odd multiples of 128 B, see make_plan).
@@ -291,45 +228,18 @@ constexpr uint32_t kLaneQuant = 256;
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
 {
-    static_assert(N >= 0 && N <= 16, "vmcnt");
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else static_assert(N == 0, "vmcnt value");
-}
-
-// XOR swizzle of a lane's 16-B pieces inside its stage slot that makes the
-// consumer's ds_read_b128 bank-conflict-free for the gfx950 lane groups (the
-// DMA writes lane-linear, so the producer applies it to the source address).
-__device__ __forceinline__ uint32_t stage_swz(uint32_t c)
-{
-    // kL pieces per lane, lane groups of ds_read_b128 (MI355X_MICROARCH.md LDS table):
-    // each group's lanes must cover distinct (bank-quad) slots.
-    return kL == 8 ? ((c >> 1) & 7u) : kL == 4 ? ((c >> 2) & 3u) : ((c >> 3) & 1u);
+    static_assert(N == 0, "vmcnt");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // One stage's kL LDS-DMA pieces in ONE asm statement: M0 is written and read
 // inside it (and restored), every VGPR offset is read before the statement
 // ends (trailing s_nop guards the compiler's next write of those registers).
-#ifndef CDC_DMA_NOPS
-#define CDC_DMA_NOPS 0
-#endif
-#if CDC_DMA_NOPS
-#define DMA_PAD "s_nop 7\n\ts_nop 7\n\t"
-#else
-#define DMA_PAD ""
-#endif
-#if CDC_DMA_NT
-#define DMA_AUX " nt"
-#else
-#define DMA_AUX ""
-#endif
-#define DMA_PIECE(i) "global_load_lds_dwordx4 %" #i ", %[base]" DMA_AUX "\n\t" DMA_PAD
+#define DMA_PIECE(i) "global_load_lds_dwordx4 %" #i ", %[base]\n\t"
 #define DMA_NEXT "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
 __device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, const uint32_t (&off)[kL])
 {
+    static_assert(kL == 4, "four 1-KiB pieces per stage");
     // wave-uniform operands pinned to SGPRs (under VGPR pressure the compiler
     // may otherwise keep them in VGPRs, which the "s" constraint does not stop);
     // the statement opens with s_nop 4 (VALU-written SGPR read as a VMEM base)
@@ -337,30 +247,12 @@ __device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, con
                           uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(base_in)));
     const uint32_t dst = __builtin_amdgcn_readfirstlane(dst_in);
     uint32_t keep;
-    if constexpr (kL == 8) {
-        asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
-                     DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4) DMA_NEXT
-                     DMA_PIECE(5) DMA_NEXT DMA_PIECE(6) DMA_NEXT DMA_PIECE(7) DMA_NEXT DMA_PIECE(8)
-                     "s_mov_b32 m0, %[keep]\n\ts_nop 1"
-                     : [keep] "=&s"(keep)
-                     : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
-                       "v"(off[7]), [base] "s"(base), [dst] "s"(dst)
-                     : "memory", "scc");
-    } else if constexpr (kL == 4) {
-        asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
-                     DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4)
-                     "s_mov_b32 m0, %[keep]\n\ts_nop 1"
-                     : [keep] "=&s"(keep)
-                     : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), [base] "s"(base), [dst] "s"(dst)
-                     : "memory", "scc");
-    } else {
-        asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
-                     DMA_PIECE(1) DMA_NEXT DMA_PIECE(2)
-                     "s_mov_b32 m0, %[keep]\n\ts_nop 1"
-                     : [keep] "=&s"(keep)
-                     : "v"(off[0]), "v"(off[1]), [base] "s"(base), [dst] "s"(dst)
-                     : "memory", "scc");
-    }
+    asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+                 DMA_PIECE(1) DMA_NEXT DMA_PIECE(2) DMA_NEXT DMA_PIECE(3) DMA_NEXT DMA_PIECE(4)
+                 "s_mov_b32 m0, %[keep]\n\ts_nop 1"
+                 : [keep] "=&s"(keep)
+                 : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), [base] "s"(base), [dst] "s"(dst)
+                 : "memory", "scc");
 }
 
 __device__ __forceinline__ uint32_t scan_wave_max(uint32_t v)
@@ -381,9 +273,6 @@ __device__ __forceinline__ uint32_t rec_ent(uint64_t rec, uint32_t e)
 // one coalesced 8-byte store per run, no atomics.
 __device__ __forceinline__ void record_hit(uint64_t &rec, int32_t r)
 {
-#if CDC_DIAG_NO_APPEND
-    if (r != 0x7FFFFFF0) return;
-#endif
     const uint32_t c = rec_cnt(rec);
     if (c < kRunCap) rec |= uint64_t(uint32_t(r)) << (kRecCntBits + kRecEntBits * c);
     if (c < (1u << kRecCntBits) - 1) ++rec;
@@ -429,17 +318,11 @@ __device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16
 // trip) and decides each 64-run word with one lane per run and one ballot.
 // It only decides where the index is built: a walker that
 // finds no index for a task raw-scans it, so results never depend on it.
-#ifndef CDC_MASKL_SPILL
-#define CDC_MASKL_SPILL 16
-#endif
-constexpr uint64_t kMaskLSpill = CDC_MASKL_SPILL;  // MaskS runs after a long stretch's end
+constexpr uint64_t kMaskLSpill = 16;  // MaskS runs after a long stretch's end (64: -1 %, 160: -11 % on C3)
 
 __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace &W, const BufDesc &D, uint64_t t,
                              uint32_t lane)
 {
-#if CDC_DIAG_MASKL_TEST == 1
-    return false;
-#endif
     const uint64_t sl = B.scan_lane, tb = 64ull * sl;
     const uint64_t start = t * tb, end = min(D.len, start + tb);
     const uint64_t ra = start / sl, rb = (end - 1) / sl;  // the task's runs
@@ -461,10 +344,6 @@ __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace
             if (r0 > rb) break;
             const uint64_t E = __ballot(rec_cnt(rec[j]) == 0);
             const uint32_t n = uint32_t(min(rb + 1 - r0, uint64_t(64)));
-#if CDC_DIAG_MASKL_TEST == 2
-            if (E == 0x123456789ull + n) return true;
-            continue;
-#endif
             // Lane i looks at run r = r0 + i: the empty stretch ending at
             // r - 1 has `prev` runs (from the word's non-empty runs Z below
             // i, or cur + i when there are none).  An empty run needs the
@@ -511,8 +390,7 @@ template <bool kMaskL, bool kFused = false>
 __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
     static_assert(!(kMaskL && kFused), "k_scan_f builds both indexes in the MaskS frame");
-    static_assert(!kFused || CDC_SCAN_V2, "k_scan_f needs the v2 staging");
-    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kNBuf * kStageBytes];
+    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kStageBytes];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
@@ -563,22 +441,25 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     // Staging starts kLead bytes before the run (>= W - 1 warm-up bytes); with
     // pair staging 128, so that its 128-B DMA chunks are whole HBM lines on a
     // 128-B aligned buffer (64-B aligned chunks straddle two lines: 40 % slower).
-    constexpr uint32_t kLead = CDC_SCAN_PAIRS ? 128u : 64u;
+    constexpr uint32_t kLead = 128u;
     const uint32_t T = uint32_t((sl + kLead + (ub & 15u) + kStage - 1u) / kStage);
     const uint64_t wb = ((ub + seg0 * sl) & ~15ull) - kLead;  // lane 0's first stage
     const uint64_t base = wb > lo_ok ? wb : lo_ok;           // wave-uniform DMA base
     const uint64_t limw = hi_ok - 16u - base;                // last in-bounds piece (lane 0 is in bounds)
     const uint32_t lim = limw > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(limw);
-    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kNBuf * kStageBytes;
-#if CDC_SCAN_V2
-    // Pair staging (see the note below for the 8 runs x 128 B DMA shape) with
-    // a register ping-pong instead of copies: even stages roll from A, odd
+    const uint32_t ring = uint32_t(reinterpret_cast<uintptr_t>(s_lds)) + kGearLdsBytes + wave * kStageBytes;
+    // Pair staging: DMA t carries 128 B (whole HBM lines) of each of the 32
+    // runs of half t & 1 of the wave (4 instructions of 8 runs x 128 B), which
+    // reads HBM ~14 % faster than 16 runs x 64 B (tools/ubench_mem.hip); half 1
+    // runs one stage behind half 0.  Slot layout: run row r = lane & 31 at
+    // 128 r, piece p at 16 (p ^ ((r >> 1) & 7)) (conflict-free ds_read_b128).
+    // A register ping-pong instead of copies: even stages roll from A, odd
     // stages from Bv.  The half that loads at stage u (u & 1) reads its 128-B
     // row once, the first 64 B into stage u's array and the second 64 B into
     // the other array (stage u + 1's); the other half reads nothing.  The DMA
     // base advances in SGPRs (per-lane offsets fixed); only a wave whose
     // pieces could leave the buffer takes the clamped form.
-    static_assert(kStage == 64 && kL == 4 && kNBuf == 1, "v2 staging: 64-B stages, one slot");
+    static_assert(kStage == 64 && kL == 4, "pair staging: 64-B stages, one slot");
     const uint32_t half = lane >> 5;
     const uint32_t row = lane & 31u, swz = (row >> 1) & 7u;
     // Half 1's runs are 32 runs after half 0's (lane lengths are multiples of
@@ -660,15 +541,6 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             const uint4 nx = gi + 1 < kGroups ? cur_d[gi + 1] : nxt_d[0];
             uint64_t (&cg)[16] = gv[gi & 1];
             uint64_t (&ng)[16] = gv[(gi + 1) & 1];
-#if CDC_DIAG_NO_COMPUTE
-            fp += nx.x ^ cur_d[gi].w;  // diagnostic: staging only
-            if (fp == 0x123456789ull) rec = fp;
-            if (gi + 1 == kGroups && t + 2 < TT) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                issue(PC, t + 2);
-            }
-            continue;
-#endif
             const uint64_t f0 = fp;
             uint32_t acc = 0xFFFFFFFFu, accL = 0xFFFFFFFFu;
 #pragma unroll
@@ -694,11 +566,7 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
-#if CDC_DIAG_NO_RECHECK
-            if (acc == 0x12345) [[unlikely]]
-#else
             if (acc == 0) [[unlikely]]
-#endif
                 recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
             if constexpr (kFused) {
                 if (accL == 0) [[unlikely]]
@@ -711,202 +579,6 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
         stage(C0{}, t, A, Bv);
         if (t + 1 < TT) stage(C1{}, t + 1, Bv, A);
     }
-#else
-#if CDC_SCAN_PAIRS
-    // Pair staging: DMA t carries 128 B (whole lines) of each of the 32 runs
-    // of half t & 1 of the wave (4 instructions of 8 runs x 128 B), which reads
-    // HBM ~14 % faster than 16 runs x 64 B (tools/ubench_mem.hip).  Half 1 runs
-    // one stage behind half 0; a lane reloads every other stage, keeping the
-    // second 64 B in registers.  Slot layout: run row r = lane & 31 at 128 r,
-    // piece p at 16 (p ^ ((r >> 1) & 7)) (conflict-free ds_read_b128).
-    static_assert(kStage == 64 && kL == 4, "pair staging: 64-B stages");
-    const uint32_t half = lane >> 5;
-    const uint32_t row = lane & 31u, swz = (row >> 1) & 7u;
-    // per-lane piece offsets of the two halves' DMAs (separate arrays, selected
-    // by bit masks: a runtime-indexed [2][4] array went to LDS)
-    uint32_t off0[4], off1[4];
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t r = 8u * j + lane / 8u;
-        const uint32_t k = (lane % 8u) ^ ((r >> 1) & 7u);
-        off0[j] = uint32_t((((ub + (seg0 + r) * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
-        off1[j] = uint32_t((((ub + (seg0 + 32u + r) * sl) & ~15ull) - kLead + 16u * k) - base);
-#if CDC_DIAG_OLD_ADDR  // diagnostic: the 16 runs x 64 B mapping (wrong data, same timing structure)
-        {
-            const uint64_t q2 = seg0 + 16u * j + lane / 4u;
-            off0[j] = off1[j] = uint32_t((((ub + q2 * sl) & ~15ull) - kLead + 16u * (lane % 4u)) - base);
-        }
-#endif
-    }
-    auto issue = [&](uint32_t t) {
-#if CDC_DIAG_NO_DMA
-        if (t >= 2 * kNBuf) return;
-#endif
-#if CDC_DIAG_OLD_ADDR
-        const uint32_t hh = 0, adv = kStage * t, m = 0;
-#else
-        const uint32_t hh = t & 1u, adv = kStage * (t - hh), m = 0u - hh;
-#endif
-        uint32_t eff[kL];
-#pragma unroll
-        for (uint32_t j = 0; j < kL; ++j) eff[j] = min(((off1[j] & m) | (off0[j] & ~m)) + adv, lim);
-        dma_stage(base, ring + (t % kNBuf) * kStageBytes, eff);
-    };
-    uint4 hold[4] = {};
-    // data of stage t for this lane: a fresh 128 B from the slot every other stage
-    auto load_stage = [&](uint32_t t, uint4 (&dd)[kGroups]) {
-        if ((t & 1u) == half) {
-            const char *buf = s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + row * 128u;
-#pragma unroll
-            for (uint32_t g = 0; g < 4; ++g) dd[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
-#pragma unroll
-            for (uint32_t g = 0; g < 4; ++g) hold[g] = *reinterpret_cast<const uint4 *>(buf + 16u * ((g + 4) ^ swz));
-        } else {
-#pragma unroll
-            for (uint32_t g = 0; g < 4; ++g) dd[g] = hold[g];
-        }
-    };
-    const uint32_t TT = T + 1;  // half 1 runs one stage behind
-    const int32_t lag = int32_t(kStage * half);
-#else
-    // the kL pieces this lane loads: DMA j carries piece (lane % kL) ^ swz of run q = seg0 + (64/kL) j + lane/kL
-    uint32_t off[kL];
-#pragma unroll
-    for (uint32_t j = 0; j < kL; ++j) {
-        const uint64_t q = seg0 + (64u / kL) * j + lane / kL;
-        const uint32_t k = (lane % kL) ^ stage_swz(uint32_t(q - seg0));
-        off[j] = uint32_t((((ub + q * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
-    }
-    auto issue = [&](uint32_t t) {
-#if CDC_DIAG_NO_DMA
-        if (t >= kNBuf) return;  // diagnostic: compute over the first ring fill again and again
-#endif
-        uint32_t eff[kL];
-#pragma unroll
-        for (uint32_t j = 0; j < kL; ++j) eff[j] = min(off[j] + kStage * t, lim);
-        dma_stage(base, ring + (t % kNBuf) * kStageBytes, eff);
-    };
-    const uint32_t swz = stage_swz(lane);
-    auto load_stage = [&](uint32_t t, uint4 (&dd)[kGroups]) {
-        const char *buf = s_lds + kGearLdsBytes + (wave * kNBuf + t % kNBuf) * kStageBytes + lane * kStage;
-#pragma unroll
-        for (uint32_t g = 0; g < kGroups; ++g) dd[g] = *reinterpret_cast<const uint4 *>(buf + 16u * (g ^ swz));
-    };
-    const uint32_t TT = T;
-    const int32_t lag = 0;
-#endif
-    const uint32_t vhi = to_vgpr(kMaskL ? P.fl_hi : P.fs_hi);
-    const uint32_t xlo = kMaskL ? P.fl_lo : P.fs_lo, xhi = kMaskL ? P.fl_hi : P.fs_hi;
-    // buffer-relative position of this lane's first staged byte
-    const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
-
-    // Every stage's data is copied into registers (d / dn) before its slot is
-    // needed again, so slot t % kNBuf is refilled with stage t + kNBuf as soon
-    // as stage t's reads have retired (after group 0 of stage t): kNBuf stages
-    // in flight per wave with a kNBuf-slot ring.
-    for (uint32_t t = 0; t < kNBuf && t < TT; ++t) issue(t);
-    if (TT > kAhead) wait_vmcnt<kL * kAhead>();
-    else wait_vmcnt<0>();
-    uint4 d[kGroups];
-    load_stage(0, d);
-    asm volatile("" ::: "memory");  // the slot reads issue before any gather (see the lgkmcnt below)
-#if CDC_EARLY_ISSUE
-    // Early issue: a slot is refilled as soon as the wave's own reads of it
-    // have retired (LDS-DMA does not wait for earlier ds_reads; the counted
-    // lgkmcnt does), so stage t + kNBuf is in flight for ~3.5 groups instead of 2.
-    if (kNBuf < TT) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        issue(kNBuf);
-    }
-#endif
-    // gathers double-buffered by group parity: group gi rolls gv[gi & 1] while
-    // the next group's values land in gv[(gi + 1) & 1]; a recheck reads the
-    // rolled group's values from registers.
-#if CDC_GV_SINGLE
-    uint64_t gv[1][16];  // single-buffered: a recheck re-gathers (fewer VGPRs, 4 waves per SIMD)
-#else
-    uint64_t gv[2][16];
-#endif
-#pragma unroll
-    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
-    uint64_t fp = 0;
-    uint64_t rec = 0;  // this lane's run record
-    const int32_t len = int32_t(e - s);
-    const int32_t rr0 = int32_t(rel0 - s) - lag;  // run-relative position of the lane's stage-0 bytes
-    for (uint32_t t = 0; t < TT; ++t) {
-        uint4 dn[kGroups];
-#pragma unroll
-        for (uint32_t gi = 0; gi < kGroups; ++gi) {
-            if (!CDC_EARLY_ISSUE && gi == 1 && t + kNBuf < TT) {
-                // >= 16 gathers were issued after stage t's slot reads: lgkmcnt(15)
-                // retires those reads, and the slot can take stage t + kNBuf.
-                asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
-                issue(t + kNBuf);
-            }
-            if (gi + 1 == kGroups) {
-                // next stage's data: landed once at most kNBuf - 1 younger stages are in flight
-                if (t + kNBuf < TT) wait_vmcnt<kL * kAhead>();
-                else wait_vmcnt<0>();
-                load_stage(t + 1, dn);
-                asm volatile("" ::: "memory");
-            }
-            const uint4 &nx = gi + 1 < kGroups ? d[gi + 1] : dn[0];
-#if CDC_GV_SINGLE
-            uint64_t (&cur)[16] = gv[0];
-            uint64_t (&nxt)[16] = gv[0];
-#else
-            uint64_t (&cur)[16] = gv[gi & 1];
-            uint64_t (&nxt)[16] = gv[(gi + 1) & 1];
-#endif
-#if CDC_DIAG_NO_COMPUTE
-            fp += nx.x ^ d[gi].w;  // diagnostic: staging only
-            if (fp == 0x123456789ull) rec = fp;
-            continue;
-#endif
-            const uint64_t f0 = fp;
-            uint32_t acc = 0xFFFFFFFFu;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                for (int k = 4 * q; k < 4 * q + 4; k += 2) {
-                    fp = (fp << 1) + cur[k];
-                    const uint32_t k0 = uint32_t(fp >> 32) & vhi;
-                    fp = (fp << 1) + cur[k + 1];
-                    acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int k = 4 * q; k < 4 * q + 4; ++k) nxt[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
-                __builtin_amdgcn_sched_barrier(0);
-#if CDC_EARLY_ISSUE
-                if (q == 1 && gi + 1 == kGroups && t + 1 + kNBuf < TT) {
-                    // the slot reads of load_stage(t + 1) precede these 8 gathers
-                    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-                    issue(t + 1 + kNBuf);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#endif
-            }
-#if CDC_DIAG_NO_RECHECK
-            if (acc == 0x12345) [[unlikely]]
-#else
-            if (acc == 0) [[unlikely]]
-#endif
-            {
-#if CDC_GV_SINGLE
-                uint64_t g2[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) g2[k] = lds_gear(tab, gear_addr(laneoff, word_of(d[gi], k >> 2), k));
-                recheck_group(f0, g2, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
-#else
-                recheck_group(f0, cur, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
-#endif
-            }
-        }
-#pragma unroll
-        for (uint32_t g = 0; g < kGroups; ++g) d[g] = dn[g];
-    }
-#endif
     if (s < int64_t(D.len)) (kMaskL ? W.runsL : W.runs)[64ull * D.task_base + seg0 + lane] = rec;
     if constexpr (kFused) {
         if (s < int64_t(D.len)) W.runsL[64ull * D.task_base + seg0 + lane] = recL;
@@ -930,9 +602,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan_l(const Batch B, const D
 // the same fingerprint, one v_alignbit + v_and and half a v_min3 per byte.
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan_f(const Batch B, const DevParams P, const Workspace W)
 {
-#if CDC_SCAN_V2
     scan_body<false, true>(B, P, W);
-#endif
 }
 
 // DPP helpers (in-row lane shifts, no LDS round trip; ds_bpermute-based
@@ -1028,17 +698,9 @@ __global__ __launch_bounds__(64) void k_selftest_wave(const uint64_t *in, uint32
 // ---------------------------------------------------------------------------
 // Wave-cooperative next(p).
 // ---------------------------------------------------------------------------
-// The walkers' rare paths (raw scans, index runs beyond the first 64) are
-// inlined: as calls they forced 182-198 VGPRs (values kept live in
-// callee-saved registers across the call), inlined the walkers need 125-137.
-#ifndef CDC_WALK_INLINE
-#define CDC_WALK_INLINE 1
-#endif
-#if CDC_WALK_INLINE
-#define CDC_WALK_INL __forceinline__
-#else
-#define CDC_WALK_INL __noinline__
-#endif
+// The rare paths (raw scans, index runs beyond the first 64) are inlined: as
+// calls they forced more VGPRs (values kept live in callee-saved registers
+// across the call).
 
 struct WalkCtx {
     uint64_t ub;       // absolute address of byte 0
@@ -1050,18 +712,13 @@ struct WalkCtx {
     const char *tab;
     uint32_t laneoff;
     uint32_t lane;
-    uint64_t *tab32;        // workgroup's 32-copy table for long raw scans, filled on first use (or null)
-    uint32_t *tab32_ready;  // LDS flag: 1 once tab32 holds the table
     const uint64_t *gear;   // the 256-entry table in device memory
     const uint64_t *runsL;  // this buffer's MaskL index records (null: no MaskL index)
     const uint32_t *validL; // per scan task of the buffer: runsL holds its 64 records
 };
 
-#ifndef CDC_RAW_TAB32
-#define CDC_RAW_TAB32 0
-#endif
-[[maybe_unused]] constexpr uint64_t kTab32MinScan = 32768;  // raw scans at least this long fill and use tab32
-// (CDC_RAW_TAB32=1: C3 +2-4 %, but C1 -4 % from the 80-KiB walker workgroups; off)
+// (A 32-copy table for long raw scans, filled on first use: C3 +2-4 %, C1 -4 %
+// from the 80-KiB workgroups; not kept.)
 
 // First position in [lo, hi) whose fingerprint (reset to 0 before fz) hits the
 // mask, by a raw scan: lane j rolls its own kRawLaneBytes slice of a block
@@ -1109,23 +766,9 @@ __device__ uint64_t raw_scan(const WalkCtx &C, const char *tab, uint32_t laneoff
     return kNoHit;
 }
 
-__device__ CDC_WALK_INL uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
+__device__ __forceinline__ uint64_t raw_first_hit(const WalkCtx &C, uint64_t lo, uint64_t hi, uint64_t fz,
                                                uint32_t mlo, uint32_t mhi)
 {
-#if CDC_RAW_TAB32
-    if (C.tab32) {
-        const bool ready = *reinterpret_cast<volatile uint32_t *>(C.tab32_ready) != 0;
-        if (ready || hi - lo >= kTab32MinScan) {
-            if (!ready) {  // this wave fills it; identical concurrent fills by other waves are harmless
-                for (uint32_t i = C.lane; i < 256u * 32u; i += 64u) C.tab32[i] = C.gear[i >> 5];
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                if (C.lane == 0) *reinterpret_cast<volatile uint32_t *>(C.tab32_ready) = 1u;
-            }
-            return raw_scan<8>(C, reinterpret_cast<const char *>(C.tab32), (C.lane & 31u) << 3, lo, hi, fz, mlo,
-                               mhi);
-        }
-    }
-#endif
     return raw_scan<kWEntShift>(C, C.tab, C.laneoff, lo, hi, fz, mlo, mhi);
 }
 
@@ -1208,7 +851,7 @@ __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0
 }
 
 // First full-window MaskS candidate in [a, b) from the run index.
-__device__ CDC_WALK_INL uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+__device__ __forceinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
     const uint64_t rl = run_of(C, b - 1);
@@ -1226,7 +869,7 @@ __device__ CDC_WALK_INL uint64_t index_first_hit(const WalkCtx &C, const DevPara
 // every window is full): from the MaskL index for the scan tasks k_scan_l
 // built (64 records per round trip, dense runs rescanned), by a raw scan for
 // the others.
-__device__ CDC_WALK_INL uint64_t maskl_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
+__device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
     if (!C.runsL) return raw_first_hit(C, a, b, fz, P.ml_lo, P.ml_hi);
@@ -1595,8 +1238,7 @@ __device__ __forceinline__ uint32_t buf_of_seg(const Batch &B, uint32_t g)
 }
 
 __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, const Workspace &W,
-                                            const char *tab, uint64_t *tab32 = nullptr,
-                                            uint32_t *tab32_ready = nullptr)
+                                            const char *tab)
 {
     WalkCtx C;
     C.ub = reinterpret_cast<uint64_t>(D.data);
@@ -1608,8 +1250,6 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.tab = tab;
     C.lane = threadIdx.x & 63u;
     C.laneoff = (C.lane & (kWCopies - 1u)) << 3;
-    C.tab32 = tab32;
-    C.tab32_ready = tab32_ready;
     C.gear = W.gear;
     C.runsL = B.maskl_index ? W.runsL + 64ull * D.task_base : nullptr;
     C.validL = B.maskl_index ? W.validL + D.task_base : nullptr;
@@ -1715,7 +1355,7 @@ __device__ __forceinline__ void put_cut(cdc_cut *out, uint64_t off, uint64_t len
 //
 // Segment r's status is a transition of the state E: when E == r (r is on the
 // chain) E becomes conv_r + 1 and its cuts are added; otherwise nothing
-// changes.  The look-back reads the statuses 64 at a time (four windows per
+// changes.  The look-back reads the statuses 64 at a time (eight windows per
 // round trip), lane j holding segment lo + j, down to the window with the
 // nearest INCLUSIVE status, and composes the transitions of each window: by
 // a prefix sum when every one is trivial (conv_r == r: the chain entered at
@@ -1724,17 +1364,9 @@ __device__ __forceinline__ void put_cut(cdc_cut *out, uint64_t off, uint64_t len
 // F of the first kJ entries of the window above (a chain leaves a window at
 // most kJ segments past its end); a longer jump takes the slow path, q - 1's
 // own INCLUSIVE status.
-// k_resolve register budget: at most 128 VGPRs lets a resolve workgroup sit
-// beside a scan workgroup (3 waves x 128 per SIMD) on every CU, so a batch's
-// resolution never holds CUs the next batch's scan is waiting for.
-#ifndef CDC_RESOLVE_WPE
-#define CDC_RESOLVE_WPE 0
-#endif
-#if CDC_RESOLVE_WPE
-#define CDC_RESOLVE_ATTR __attribute__((amdgpu_waves_per_eu(CDC_RESOLVE_WPE)))
-#else
-#define CDC_RESOLVE_ATTR
-#endif
+// (k_resolve capped at 128 VGPRs, so that a resolve workgroup fits beside a
+// scan workgroup, spilled 153 registers: 48 us alone instead of 25, and the
+// warm pipelined C1 rate fell from 4.70k to 4.31k GiB/s.  Not kept.)
 constexpr uint32_t kJ = 8;
 constexpr uint32_t kLbWin = 8;  // windows per round trip
 
@@ -2115,9 +1747,9 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     }
 }
 
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) CDC_RESOLVE_ATTR void k_resolve(const Batch B, const DevParams P, const Workspace W)
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B, const DevParams P, const Workspace W)
 {
-    __builtin_amdgcn_s_setprio(CDC_TAIL_PRIO);  // latency-bound: issue ahead of a co-resident scan (next batch)
+    __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
     __shared__ GraphLds s_graph[kWalkWavesPerWG];
     __shared__ uint32_t s_ticket;
@@ -2257,7 +1889,7 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     // With profiling on, the events ride on the kernels' own dispatch packets
     // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
     const dim3 sgrid((B.total_tasks + kS2Waves - 1) / kS2Waves), sblock(kS2Waves * 64);
-    const bool fused = CDC_SCAN_V2 && B.maskl_index && B.maskl_fused;  // k_scan_f: both indexes in one pass
+    const bool fused = B.maskl_index && B.maskl_fused;  // k_scan_f: both indexes in one pass
     if (B.total_tasks == 0) {  // every buffer is empty
         if (prof) {
             (void)hipEventRecord(pr.e0, st);
