@@ -1,0 +1,125 @@
+"""GPU parity at the shapes the benchmark and the driver use (BASELINE.json
+configs), plus the multi-rank and multi-device paths and the sequential
+fallback's cost.  Every check is bit-exact against the CPU oracle.
+"""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from datagen import random_bytes  # noqa: E402
+from plakar_amd import _lib, chunkers, device  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEF = dict(min_size=65536, normal_size=1 << 20, max_size=4 << 20)
+OPTS = chunkers.ChunkerOpts(MinSize=65536, NormalSize=1 << 20, MaxSize=4 << 20)
+
+
+def assert_same(got, ref, what=""):
+    got = np.asarray(got).astype(np.uint64)
+    assert got.shape == ref.shape, f"{what}: {got.shape[0]} chunks vs oracle {ref.shape[0]}"
+    bad = np.nonzero((got != ref).any(axis=1))[0]
+    assert bad.size == 0, f"{what}: first mismatch at chunk {bad[0]}: {got[bad[0]]} vs {ref[bad[0]]}"
+
+
+def test_c4_full_gpu_share_host_path(oracle):
+    """BASELINE configs[4], one GPU's share exactly as bench.py builds it (the
+    first 512 files of the 4096-file Zipf corpus, seeds 1..512): chunkify
+    routing (snapshot/backup.go:631-644: files < MinSize are one chunk, no CDC),
+    the rest through cdc_chunk; every file checked against the oracle."""
+    from bench import WORKLOADS, make_host_corpus
+    _lib.ensure_init()
+    corpus = make_host_corpus(WORKLOADS["c4"], 0, 1)
+    assert len(corpus) == 512
+    big = [a for a in corpus if a.size >= DEF["min_size"]]
+    small = [a for a in corpus if a.size < DEF["min_size"]]
+    assert big and small
+    res = chunkers.ChunkBuffers(big, OPTS)
+    gear = _lib.default_gear()
+    for i, a in enumerate(big):
+        assert_same(res[i], oracle.chunk(a, gear, **DEF), f"file {i} ({a.size} B)")
+    for a in small:  # routed: one chunk, the oracle's chunkify agrees
+        ref = oracle.chunk(a, gear, chunkify=True, **DEF)
+        assert ref.shape[0] == 1 and int(ref[0, 1]) == a.size
+
+
+def test_cdc_chunk_all_visible_devices(oracle):
+    """cdc_chunk with dev_mask = 0 (every visible device, LPT over devices)."""
+    _lib.ensure_init(dev_mask=0)
+    n = _lib.lib().cdc_device_count()
+    assert n >= 1
+    bufs = [random_bytes(s, 900 + i) for i, s in enumerate([96 << 20, 5 << 20, 33 << 20, 1 << 20, 0, 200_000])]
+    res = chunkers.ChunkBuffers(bufs, OPTS)
+    gear = _lib.default_gear()
+    for i, a in enumerate(bufs):
+        assert_same(res[i], oracle.chunk(a, gear, **DEF), f"buffer {i}")
+
+
+def test_buffer_over_4GiB_host_path(oracle):
+    """One 4.5 GiB buffer through cdc_chunk (offsets past 2^32, staged whole)."""
+    _lib.ensure_init()
+    n = (4 << 30) + (512 << 20)
+    a = random_bytes(n, 4242)
+    (got,) = chunkers.ChunkBuffers([a], OPTS)
+    ref = oracle.chunk(a, _lib.default_gear(), **DEF)
+    assert int(ref[-1, 0]) > (1 << 32)
+    assert_same(got, ref, "4.5 GiB")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_c2_shares_on_one_gpu():
+    """The N-rank path of bench.py on hardware: 2 ranks (torch.distributed.run,
+    gloo), both on device 0 of a one-GPU box, each chunking its own share of
+    BASELINE configs[2] (32 x 64 MiB, bench.buffer_seeds) and checking every
+    cut list against the oracle; only a failure count crosses ranks."""
+    env = dict(os.environ, DIST_ONE_GPU="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_c2_worker.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    import json
+    d = json.loads(line)
+    assert d["ranks"] == 2 and d["buffers"] == 64 and d["mismatched_buffers"] == 0, d
+
+
+def test_sequential_fallback_cost_1GiB(oracle):
+    """The sequential fallback (debug mode 1 forces it) on a 1 GiB buffer: the
+    cliff a buffer whose speculative chains never merge would hit.  Bit-exact,
+    and its time is printed (DESIGN.md records it)."""
+    _lib.ensure_init()
+    a = random_bytes(1 << 30, 77)
+    t = torch.from_numpy(a).to("cuda")
+    L = _lib.lib()
+    try:
+        L.cdc_set_debug_mode(1)
+        b = device.DeviceBatch([t], OPTS)
+        b.launch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        b.launch()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        cuts, _ = b.results()
+    finally:
+        L.cdc_set_debug_mode(0)
+    ref = oracle.chunk(a, _lib.default_gear(), **DEF)
+    assert_same(cuts[0].cpu().numpy(), ref, "sequential 1 GiB")
+    print(f"\nsequential fallback: 1 GiB, {ref.shape[0]} chunks in {el * 1e3:.1f} ms "
+          f"({el * 1e6 / ref.shape[0]:.2f} us per chunk)")
