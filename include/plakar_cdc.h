@@ -128,6 +128,33 @@ void cdc_default_opts(cdc_opts *out);
 int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out,
               uint64_t out_cap, uint64_t *out_counts, uint64_t *out_needed);
 
+/* ---- pinned batch arena: files in, host cut lists out --------------------------
+ * Replaces the importer's per-file os.Open + bufio reads
+ * (snapshot/importer/fs/fs.go:69-71) feeding the per-file Next() loop: a
+ * batch of files is read with pread(2) straight into library-owned pinned
+ * host memory, then chunked by one cdc_chunk call whose host-to-device copies
+ * are pinned DMA.  The bytes stay in the arena (cdc_batch_get) for the
+ * per-chunk work (processChunk) until cdc_batch_reset.  A cgo caller passes
+ * only file descriptors, paths and C memory: no Go pointer is stored.
+ *   cdc_batch_new        arena of `capacity` bytes (buffers are 4-KiB aligned)
+ *   cdc_batch_reserve    append a buffer of len bytes; *ptr = where to write it
+ *   cdc_batch_add_fd     append len bytes read from fd (pread from offset 0)
+ *   cdc_batch_add_files  append n whole files, read by `threads` threads;
+ *                        sizes[i] = file sizes (may be NULL).  All or nothing.
+ *   cdc_batch_chunk      cdc_chunk over the arena's buffers, in order
+ * Errors: CDC_E_NOSPACE (arena full), CDC_E_IO, CDC_E_NOT_INIT. */
+typedef struct cdc_batch cdc_batch;
+int cdc_batch_new(uint64_t capacity, cdc_batch **out);
+int cdc_batch_reserve(cdc_batch *b, uint64_t len, uint8_t **ptr);
+int cdc_batch_add_fd(cdc_batch *b, int fd, uint64_t len);
+int cdc_batch_add_files(cdc_batch *b, const char *const *paths, int n, int threads, uint64_t *sizes);
+int cdc_batch_count(const cdc_batch *b);
+int cdc_batch_get(const cdc_batch *b, int i, const uint8_t **ptr, uint64_t *len);
+int cdc_batch_chunk(cdc_batch *b, const cdc_opts *opts, cdc_cut *out, uint64_t out_cap,
+                    uint64_t *out_counts, uint64_t *out_needed);
+void cdc_batch_reset(cdc_batch *b);
+void cdc_batch_free(cdc_batch *b);
+
 /* ---- device-resident path -----------------------------------------------------
  * d_data: device pointer to len bytes (any alignment) on `device`.
  * final != 0: the buffer is a whole stream, so the last chunk ends at len.

@@ -101,6 +101,17 @@ SIGNATURES = {
                                                             _P(ctypes.c_void_p), _P(ctypes.c_uint64),
                                                             _P(ctypes.c_void_p), _P(ctypes.c_void_p),
                                                             _P(ctypes.c_void_p), ctypes.c_void_p]),
+    "cdc_batch_new": (ctypes.c_int, [ctypes.c_uint64, _P(ctypes.c_void_p)]),
+    "cdc_batch_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, _P(_P(ctypes.c_uint8))]),
+    "cdc_batch_add_fd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]),
+    "cdc_batch_add_files": (ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_char_p), ctypes.c_int, ctypes.c_int,
+                                           _P(ctypes.c_uint64)]),
+    "cdc_batch_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "cdc_batch_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _P(_P(ctypes.c_uint8)), _P(ctypes.c_uint64)]),
+    "cdc_batch_chunk": (ctypes.c_int, [ctypes.c_void_p, _P(cdc_opts), _P(cdc_cut), ctypes.c_uint64,
+                                       _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
+    "cdc_batch_reset": (None, [ctypes.c_void_p]),
+    "cdc_batch_free": (None, [ctypes.c_void_p]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),

@@ -50,7 +50,25 @@ def build_oracle(verbose=True):
     return os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 
 
+def build_ctests(verbose=True):
+    """Compile the C-level boundary test (tests/c/abi_threads.c) against the
+    library and the CPU oracle (its checker) into tests/_build/."""
+    out_dir = os.path.join(ROOT, "tests", "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    exe = os.path.join(out_dir, "abi_threads")
+    src = [os.path.join(ROOT, "tests", "c", "abi_threads.c"), os.path.join(ROOT, "oracle", "fastcdc_oracle.c")]
+    if not _stale(exe, src + [LIB] + HEADERS):
+        return exe
+    cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-I", os.path.join(ROOT, "include"), "-o", exe] + src + \
+          ["-L", LIB_DIR, "-lplakar_cdc", "-Wl,-rpath,$ORIGIN/../../plakar_amd/_lib", "-lpthread"]
+    if verbose:
+        print("[plakar_amd.build]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return exe
+
+
 if __name__ == "__main__":
     build_lib(force="--force" in sys.argv)
     if "--lib-only" not in sys.argv:
         build_oracle()
+        build_ctests()

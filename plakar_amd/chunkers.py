@@ -12,6 +12,7 @@ chunked by the device kernels; ChunkBuffers is the batch form used by the
 re-plumbed backup (one call for many files).
 """
 import ctypes
+import os
 
 from . import _lib
 from ._lib import CDC_EOF, CDC_NEED_DATA, CDC_OK, CdcError, check, ensure_init, lib
@@ -176,3 +177,82 @@ def ChunkBuffers(bufs, opts):
         res.append(part)
         k += c
     return res
+
+
+class FileBatch:
+    """A batch of whole files read straight into library-owned pinned host
+    memory (cdc_batch_*), chunked in one call with pinned host-to-device
+    copies.  This is the importer side of the re-plumbed backup: plakar opens
+    and reads each file (snapshot/importer/fs/fs.go:69-71) and chunks it
+    (snapshot/backup.go:647-665); here a whole batch of files is read by
+    `threads` threads into the arena and chunked at once.  The bytes stay
+    readable (`buffer(i)`) until `reset()`, for the per-chunk work."""
+
+    def __init__(self, capacity):
+        ensure_init()
+        self._h = ctypes.c_void_p()
+        check(lib().cdc_batch_new(int(capacity), ctypes.byref(self._h)), "cdc_batch_new")
+
+    def add_files(self, paths, threads=8):
+        """Append whole files (all or none); returns their sizes."""
+        n = len(paths)
+        arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        sizes = (ctypes.c_uint64 * max(n, 1))()
+        check(lib().cdc_batch_add_files(self._h, arr, n, int(threads), sizes), "cdc_batch_add_files")
+        return [int(sizes[i]) for i in range(n)]
+
+    def add_fd(self, fd, length):
+        check(lib().cdc_batch_add_fd(self._h, int(fd), int(length)), "cdc_batch_add_fd")
+
+    def __len__(self):
+        return lib().cdc_batch_count(self._h)
+
+    def buffer(self, i):
+        """The bytes of buffer i (a numpy view of the pinned arena; valid until reset())."""
+        import numpy as np
+        ptr = ctypes.POINTER(ctypes.c_uint8)()
+        ln = ctypes.c_uint64()
+        check(lib().cdc_batch_get(self._h, int(i), ctypes.byref(ptr), ctypes.byref(ln)), "cdc_batch_get")
+        if ln.value == 0:
+            return np.zeros(0, dtype=np.uint8)
+        return np.ctypeslib.as_array(ptr, shape=(ln.value,))
+
+    def chunk(self, opts):
+        """cdc_chunk over every buffer: per buffer a uint64 (n, 2) array of (offset, length) rows."""
+        import numpy as np
+        o = opts._c()
+        check(lib().cdc_validate(b"fastcdc", ctypes.byref(o)), "FileBatch.chunk")
+        n = len(self)
+        total = 0
+        for i in range(n):
+            ptr = ctypes.POINTER(ctypes.c_uint8)()
+            ln = ctypes.c_uint64()
+            check(lib().cdc_batch_get(self._h, i, ctypes.byref(ptr), ctypes.byref(ln)))
+            total += ln.value // max(opts.MinSize, 1) + 2
+        out = np.zeros((max(total, 1), 2), dtype=np.uint64)
+        counts = (ctypes.c_uint64 * max(n, 1))()
+        needed = ctypes.c_uint64()
+        check(lib().cdc_batch_chunk(self._h, ctypes.byref(o), ctypes.cast(out.ctypes.data, ctypes.POINTER(_lib.cdc_cut)),
+                                    out.shape[0], counts, ctypes.byref(needed)), "FileBatch.chunk")
+        res, k = [], 0
+        for i in range(n):
+            c = counts[i]
+            part = out[k:k + c].copy()
+            part[:, 1] &= np.uint64(0xFFFFFFFF)
+            res.append(part)
+            k += c
+        return res
+
+    def reset(self):
+        lib().cdc_batch_reset(self._h)
+
+    def close(self):
+        if self._h:
+            lib().cdc_batch_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

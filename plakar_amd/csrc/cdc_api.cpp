@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,10 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "cdc_internal.h"
 
@@ -905,6 +910,146 @@ int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out
 }
 
 }  // extern "C"
+
+// ===========================================================================
+// Pinned batch arena: files read straight into library-owned pinned memory
+// (the importer's os.Open + read, snapshot/importer/fs/fs.go:69-71), then one
+// cdc_chunk over them (pinned hipMemcpyAsync, no staging copy).  A cgo caller
+// hands the library only C memory and file descriptors, never a Go pointer to
+// keep.
+// ===========================================================================
+struct cdc_batch {
+    uint8_t *base = nullptr;
+    uint64_t cap = 0, used = 0;
+    std::vector<cdc_buf> bufs;
+};
+
+static constexpr uint64_t kBatchAlign = 4096;
+
+extern "C" int cdc_batch_new(uint64_t capacity, cdc_batch **out)
+{
+    if (!out) return CDC_E_INVALID;
+    *out = nullptr;
+    if (!G().init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
+    auto *b = new cdc_batch();
+    b->cap = (capacity + kBatchAlign - 1) & ~(kBatchAlign - 1);
+    if (b->cap && hipHostMalloc(reinterpret_cast<void **>(&b->base), b->cap, hipHostMallocPortable) != hipSuccess) {
+        delete b;
+        return CDC_E_NOMEM;
+    }
+    *out = b;
+    return CDC_OK;
+}
+
+extern "C" int cdc_batch_reserve(cdc_batch *b, uint64_t len, uint8_t **ptr)
+{
+    if (!b || !ptr) return CDC_E_INVALID;
+    const uint64_t need = (len + kBatchAlign - 1) & ~(kBatchAlign - 1);
+    if (need > b->cap - b->used) return CDC_E_NOSPACE;
+    *ptr = b->base + b->used;
+    b->bufs.push_back(cdc_buf{len ? b->base + b->used : nullptr, len});
+    b->used += need;
+    return CDC_OK;
+}
+
+static int read_full(int fd, uint8_t *dst, uint64_t len)
+{
+    uint64_t got = 0;
+    while (got < len) {
+        const ssize_t k = pread(fd, dst + got, size_t(std::min<uint64_t>(len - got, 1ull << 30)), off_t(got));
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return CDC_E_IO;
+        got += uint64_t(k);
+    }
+    return CDC_OK;
+}
+
+extern "C" int cdc_batch_add_fd(cdc_batch *b, int fd, uint64_t len)
+{
+    uint8_t *p = nullptr;
+    const int st = cdc_batch_reserve(b, len, &p);
+    if (st != CDC_OK) return st;
+    const int r = read_full(fd, p, len);
+    if (r != CDC_OK) {  // drop the slot again
+        b->bufs.pop_back();
+        b->used = uint64_t(p - b->base);
+    }
+    return r;
+}
+
+extern "C" int cdc_batch_add_files(cdc_batch *b, const char *const *paths, int n, int threads, uint64_t *sizes)
+{
+    if (!b || n < 0 || (n > 0 && !paths)) return CDC_E_INVALID;
+    const size_t first = b->bufs.size();
+    const uint64_t used0 = b->used;
+    std::vector<int> fds(size_t(n), -1);
+    auto undo = [&](int st) {
+        for (int fd : fds)
+            if (fd >= 0) close(fd);
+        b->bufs.resize(first);
+        b->used = used0;
+        return st;
+    };
+    for (int i = 0; i < n; ++i) {
+        struct stat sb;
+        fds[size_t(i)] = open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fds[size_t(i)] < 0 || fstat(fds[size_t(i)], &sb) != 0) return undo(CDC_E_IO);
+        uint8_t *p = nullptr;
+        const int st = cdc_batch_reserve(b, uint64_t(sb.st_size), &p);
+        if (st != CDC_OK) return undo(st);
+        if (sizes) sizes[i] = uint64_t(sb.st_size);
+    }
+    const int nt = std::max(1, std::min(threads, n));
+    std::atomic<int> next{0}, err{CDC_OK};
+    auto work = [&] {
+        for (int i; (i = next.fetch_add(1)) < n;) {
+            const cdc_buf &cb = b->bufs[first + size_t(i)];
+            const int st = read_full(fds[size_t(i)], static_cast<uint8_t *>(const_cast<void *>(cb.data)), cb.len);
+            if (st != CDC_OK) err.store(st);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    if (err.load() != CDC_OK) return undo(err.load());
+    for (int &fd : fds) {
+        close(fd);
+        fd = -1;
+    }
+    return CDC_OK;
+}
+
+extern "C" int cdc_batch_count(const cdc_batch *b) { return b ? int(b->bufs.size()) : 0; }
+
+extern "C" int cdc_batch_get(const cdc_batch *b, int i, const uint8_t **ptr, uint64_t *len)
+{
+    if (!b || i < 0 || size_t(i) >= b->bufs.size() || !ptr || !len) return CDC_E_INVALID;
+    *ptr = static_cast<const uint8_t *>(b->bufs[size_t(i)].data);
+    *len = b->bufs[size_t(i)].len;
+    return CDC_OK;
+}
+
+extern "C" int cdc_batch_chunk(cdc_batch *b, const cdc_opts *opts, cdc_cut *out, uint64_t out_cap,
+                               uint64_t *out_counts, uint64_t *out_needed)
+{
+    if (!b) return CDC_E_INVALID;
+    return cdc_chunk(b->bufs.data(), int(b->bufs.size()), opts, out, out_cap, out_counts, out_needed);
+}
+
+extern "C" void cdc_batch_reset(cdc_batch *b)
+{
+    if (!b) return;
+    b->bufs.clear();
+    b->used = 0;
+}
+
+extern "C" void cdc_batch_free(cdc_batch *b)
+{
+    if (!b) return;
+    if (b->base) (void)hipHostFree(b->base);
+    delete b;
+}
 
 // ===========================================================================
 // Streaming chunker: ext go-cdc-chunkers (*Chunker).Next over a pinned window.

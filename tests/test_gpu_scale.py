@@ -123,3 +123,30 @@ def test_sequential_fallback_cost_1GiB(oracle):
     assert_same(cuts[0].cpu().numpy(), ref, "sequential 1 GiB")
     print(f"\nsequential fallback: 1 GiB, {ref.shape[0]} chunks in {el * 1e3:.1f} ms "
           f"({el * 1e6 / ref.shape[0]:.2f} us per chunk)")
+
+
+def test_file_batch_pinned_arena(oracle, tmp_path):
+    """Files read by the library (pread, 8 threads) into its pinned arena, then
+    one cdc_batch_chunk; bytes and cut lists checked against the files and the
+    oracle (snapshot/importer/fs/fs.go:69-71 + snapshot/backup.go:647-665)."""
+    _lib.ensure_init()
+    sizes = [0, 1, 65535, 65536, 3 << 20, (17 << 20) + 5, 40 << 20, 123_457]
+    paths, datas = [], []
+    for i, n in enumerate(sizes):
+        a = random_bytes(n, 700 + i)
+        p = tmp_path / f"f{i}"
+        p.write_bytes(a.tobytes())
+        paths.append(str(p))
+        datas.append(a)
+    fb = chunkers.FileBatch(sum((n + 4095) // 4096 * 4096 for n in sizes))
+    assert fb.add_files(paths, threads=8) == sizes
+    assert len(fb) == len(sizes)
+    for i, a in enumerate(datas):
+        assert np.array_equal(fb.buffer(i), a)
+    res = fb.chunk(OPTS)
+    gear = _lib.default_gear()
+    for i, a in enumerate(datas):
+        assert_same(res[i], oracle.chunk(a, gear, **DEF), f"file {i}")
+    fb.reset()
+    assert len(fb) == 0
+    fb.close()
