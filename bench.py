@@ -39,6 +39,10 @@ WORKLOADS = {
     "c4": dict(desc="C4: Zipf(1.1) corpus of 4 KiB-128 MiB files, 512 per GPU (BASELINE configs[4], one GPU's "
                     "share), host buffers in -> cut lists in host memory (PCIe-inclusive)",
                nbuf=512, size=0, kind="zipf", host=True),
+    "c4f": dict(desc="C4 from files: the same 512-file share written to disk once (untimed), then per step read by the "
+                     "library (pread, 16 threads) into its pinned arena and chunked (pinned H2D, cut lists to host); "
+                     "warm page cache",
+                nbuf=512, size=0, kind="zipf", host=True, files=True),
 }
 
 
@@ -308,6 +312,23 @@ def main():
 
         def step():
             return chunkers.ChunkBuffers(host_bufs, opts)
+
+        if wl.get("files"):
+            import tempfile
+            tmpdir = tempfile.mkdtemp(prefix="cdc_c4f_")
+            paths = []
+            for i, a in enumerate(host_bufs):
+                pth = os.path.join(tmpdir, f"f{i:04d}")
+                with open(pth, "wb") as f:
+                    f.write(a.tobytes())
+                paths.append(pth)
+            del corpus
+            fbatch = chunkers.FileBatch(sum((a.size + 4095) // 4096 * 4096 for a in host_bufs))
+
+            def step():
+                fbatch.reset()
+                fbatch.add_files(paths, threads=16)
+                return fbatch.chunk(opts)
     else:
         size = (args.size_mib << 20) if args.size_mib else wl["size"]
         bufs = make_buffers(torch, wl, rank, dev, size, world)
@@ -417,7 +438,9 @@ def main():
                   "chunks_per_step": nchunks}
         if host_mode:
             config["routed_bytes_per_gpu"] = routed_bytes
-            config["timing"] = "end-to-end incl. host->device copies and cut lists back to host"
+            config["timing"] = ("end-to-end incl. file reads into pinned memory, host->device copies and cut lists back "
+                            "to host" if wl.get("files") else
+                            "end-to-end incl. host->device copies and cut lists back to host")
         else:
             config["streams"] = nstreams
             config["timing"] = ("K independent passes over the input, each a full chunking of every buffer into "
@@ -439,6 +462,10 @@ def main():
             "chunk_digests": digest,
         }
         print(json.dumps(line), flush=True)
+    if host_mode and wl.get("files"):
+        import shutil
+        fbatch.close()
+        shutil.rmtree(tmpdir, ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
     sys.stdout.flush()
