@@ -128,6 +128,33 @@ void cdc_default_opts(cdc_opts *out);
 int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out,
               uint64_t out_cap, uint64_t *out_counts, uint64_t *out_needed);
 
+/* ---- packfile builder: the consumer of the cut lists ---------------------------
+ * snapshot/packer.go + packfile/packfile.go: blobs are appended to a
+ * packfile whose bytes are those of (*PackFile).Serialize (packfile.go:241-294):
+ * Blobs, then per blob {u8 type, 32-B checksum, u32 offset, u32 length}, then
+ * the footer {u32 version 100, i64 timestamp, u32 count, u32 index offset,
+ * 32-B SHA-256 of the index}, all little-endian.
+ *   cdc_packer_add_blob    Packer.AddBlob; returns 1 once Size() > MaxSize
+ *                          (packerJob's flush rule, snapshot/snapshot.go:71)
+ *   cdc_packer_add_chunks  TYPE_CHUNK blobs base[cuts[i]] with digests[32 i]
+ *                          (k_chunk_digest's output), rows with skip[i] != 0
+ *                          skipped (BlobExists); stops after the blob that
+ *                          fills the packfile; returns rows consumed
+ *   cdc_packer_serialize   the whole packfile; _part: 0 data, 1 index,
+ *                          2 footer (PutPackfile Encode's index and footer) */
+typedef struct cdc_packer cdc_packer;
+int cdc_packer_new(uint32_t max_size, cdc_packer **out);
+int cdc_packer_add_blob(cdc_packer *p, uint8_t type, const uint8_t checksum[32], const uint8_t *data, uint64_t len);
+int64_t cdc_packer_add_chunks(cdc_packer *p, const uint8_t *base, const cdc_cut *cuts, uint64_t n,
+                              const uint8_t *digests, const uint8_t *skip);
+uint64_t cdc_packer_size(const cdc_packer *p);
+uint32_t cdc_packer_count(const cdc_packer *p);
+int cdc_packer_serialize(const cdc_packer *p, int64_t timestamp, uint8_t *out, uint64_t cap, uint64_t *len);
+int cdc_packer_serialize_part(const cdc_packer *p, int part, int64_t timestamp, uint8_t *out, uint64_t cap,
+                              uint64_t *len);
+void cdc_packer_reset(cdc_packer *p);
+void cdc_packer_free(cdc_packer *p);
+
 /* ---- pinned batch arena: files in, host cut lists out --------------------------
  * Replaces the importer's per-file os.Open + bufio reads
  * (snapshot/importer/fs/fs.go:69-71) feeding the per-file Next() loop: a

@@ -112,6 +112,19 @@ SIGNATURES = {
                                        _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
     "cdc_batch_reset": (None, [ctypes.c_void_p]),
     "cdc_batch_free": (None, [ctypes.c_void_p]),
+    "cdc_packer_new": (ctypes.c_int, [ctypes.c_uint32, _P(ctypes.c_void_p)]),
+    "cdc_packer_add_blob": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, _P(ctypes.c_uint8), ctypes.c_void_p,
+                                           ctypes.c_uint64]),
+    "cdc_packer_add_chunks": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, _P(cdc_cut), ctypes.c_uint64,
+                                               ctypes.c_void_p, ctypes.c_void_p]),
+    "cdc_packer_size": (ctypes.c_uint64, [ctypes.c_void_p]),
+    "cdc_packer_count": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "cdc_packer_serialize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint64,
+                                            _P(ctypes.c_uint64)]),
+    "cdc_packer_serialize_part": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                                 ctypes.c_uint64, _P(ctypes.c_uint64)]),
+    "cdc_packer_reset": (None, [ctypes.c_void_p]),
+    "cdc_packer_free": (None, [ctypes.c_void_p]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),

@@ -26,10 +26,17 @@ parts (cuts, checksums, counts) are exact.
 Chunk.Distribution and Object.Distribution are float64 numpy rows of 256
 (the Go [256]float64 arrays).
 
+backup_batch adds the consumer side: every
+chunk not stored yet (BlobExists, backup.go:625) goes through PutBlob
+(blobs.go:11-26: Encode, then the packer channel) into packfiles built by the
+native packer (packer.py over cdc_packer_*, snapshot/packer.go and
+packfile/packfile.go), flushed at Size() > MaxSize as packerJob does
+(snapshot/snapshot.go:51-92).
+
 Out of scope, as in SURVEY.md: the content type (mime detection), the
-classifier, the blob dedup and PutBlob / packer (storage), and the
-object's Distribution (the reference never assigns it from its running
-total: backup.go:668-677 leaves it zero).
+classifier, the repository state and storage backends, and the object's
+Distribution (the reference never assigns it from its running total:
+backup.go:668-677 leaves it zero).
 
 The per-object SHA-256 is one serial chain per file.  On the device it is one
 lane per file, ~32 MB/s per lane: it pays for many small files hashed
@@ -159,4 +166,49 @@ def chunkify_batch(files, repo: Repository = None, dev=0, object_hash="auto", de
     return objects
 
 
-__all__ = ["Object", "route", "chunkify_batch"]
+def backup_batch(files, repo: Repository = None, known=None, max_size=None, encode=None, timestamp=None, **kw):
+    """chunkify_batch, then PutBlob of every new chunk into packfiles.
+
+    known: set of chunk checksums already stored (BlobExists); updated.
+    encode: Repository.Encode (compression, then encryption:
+    repository/repository.go:212-236) applied to each blob before it is
+    packed, as PutBlob does; None = no compression / no encryption.
+    Returns (objects, packfiles): the Object records and the serialised
+    packfiles (packfile.go Serialize form)."""
+    from . import packer as packer_mod
+    max_size = packer_mod.DEFAULT_MAX_SIZE if max_size is None else int(max_size)
+    known = set() if known is None else known
+    objects = chunkify_batch(files, repo, **kw)
+    arrs = [np.frombuffer(f, dtype=np.uint8) if not isinstance(f, np.ndarray) else np.ascontiguousarray(f, np.uint8)
+            for f in files]
+    if encode is None:  # the native path: cut rows and digests straight into the packer
+        cut_lists, digest_lists, keep = [], [], []
+        for a, obj in zip(arrs, objects):
+            lens = np.array([c.Length for c in obj.Chunks], dtype=np.uint64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if lens.size else lens
+            cut_lists.append(np.stack([offs, lens], axis=1) if lens.size else np.zeros((0, 2), np.uint64))
+            digest_lists.append(np.frombuffer(b"".join(c.Checksum for c in obj.Chunks), dtype=np.uint8))
+            keep.append(a)
+        packs = packer_mod.pack_chunks(keep, cut_lists, digest_lists, max_size=max_size, known=known,
+                                       timestamp=timestamp)
+        return objects, packs
+    packs = []
+    pk = packer_mod.Packer(max_size, timestamp)
+    for a, obj in zip(arrs, objects):
+        off = 0
+        for c in obj.Chunks:
+            data = a[off:off + c.Length]
+            off += c.Length
+            if c.Checksum in known:
+                continue
+            known.add(c.Checksum)
+            if pk.AddBlob(packer_mod.TYPE_CHUNK, c.Checksum, encode(data.tobytes())):
+                packs.append(pk.Serialize())
+                pk.Reset()
+    if pk.Count():
+        packs.append(pk.Serialize())
+    pk.close()
+    return objects, packs
+
+
+__all__ = ["Object", "route", "chunkify_batch", "backup_batch"]

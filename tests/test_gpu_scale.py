@@ -150,3 +150,41 @@ def test_file_batch_pinned_arena(oracle, tmp_path):
     fb.reset()
     assert len(fb) == 0
     fb.close()
+
+
+def test_backup_batch_packfiles(oracle):
+    """chunkify on the device -> PutBlob of every new chunk -> packfiles (the
+    re-plumbed snapshot/backup.go:594-629 + snapshot/packer.go): each packfile
+    parses as packfile.go's format (tests/packfile_ref.py), every new chunk is
+    stored once, already-known ones are skipped, and every blob is Encode(the
+    file's bytes at the device cut) with that chunk's SHA-256 as its key."""
+    import hashlib
+    import zlib
+
+    import packfile_ref as ref
+    from plakar_amd import snapshot
+    _lib.ensure_init()
+    files = [random_bytes(n, 60 + i) for i, n in enumerate([0, 1000, 70_000, 5 << 20, 9 << 20, 33 << 20])]
+    files.append(files[3].copy())  # duplicate content: deduplicated
+    gear = _lib.default_gear()
+    want = {}
+    for f in files:
+        rows = oracle.chunk(f, gear, chunkify=True, **DEF) if f.size else np.array([[0, 0]], np.uint64)
+        for o, n in rows:
+            data = f[int(o):int(o + n)].tobytes()
+            want[hashlib.sha256(data).digest()] = data
+    first = next(iter(want))
+    for encode in (None, lambda b: zlib.compress(b, 1)):
+        known = {first}
+        objs, packs = snapshot.backup_batch(files, known=set(known), max_size=8 << 20, encode=encode, timestamp=5)
+        assert len(objs) == len(files)
+        got = {}
+        for pk in packs:
+            pf = ref.parse(pk)
+            assert pf.timestamp == 5
+            for t, c, o, n in pf.index:
+                assert t == ref.TYPE_CHUNK and c not in got
+                got[c] = bytes(pf.blobs[o:o + n])
+        assert set(got) == set(want) - {first}
+        for c, blob in got.items():
+            assert blob == (want[c] if encode is None else zlib.compress(want[c], 1))
