@@ -20,7 +20,8 @@ class Packer:
     def __init__(self, max_size=DEFAULT_MAX_SIZE, timestamp=None):
         self._h = ctypes.c_void_p()
         check(lib().cdc_packer_new(int(max_size), ctypes.byref(self._h)), "cdc_packer_new")
-        self.timestamp = time.time_ns() if timestamp is None else int(timestamp)  # packfile.New
+        self._fixed = timestamp is not None  # a fixed Footer.Timestamp (tests); else packfile.New's time.Now()
+        self.timestamp = time.time_ns() if timestamp is None else int(timestamp)
 
     def AddBlob(self, typ, checksum, data):
         """Packer.AddBlob; returns True once Size() > MaxSize (packerJob then flushes)."""
@@ -79,7 +80,8 @@ class Packer:
 
     def Reset(self):
         lib().cdc_packer_reset(self._h)
-        self.timestamp = time.time_ns()
+        if not self._fixed:
+            self.timestamp = time.time_ns()
 
     def close(self):
         if self._h:
