@@ -183,6 +183,41 @@ def digest_leg(torch, batch, bufs, reps, check):
     return d
 
 
+def chunk_digest_pipeline(torch, bufs, opts, dev, nstreams, passes):
+    """Chunking + per-chunk SHA-256 and histograms (processChunk's device work,
+    snapshot/backup.go:594-629) as a backup streams batches: each pass chunks
+    the rank's buffers, then hashes every chunk, on its own stream; `nstreams`
+    passes are in flight at once, so one pass's digests (a serial chain per
+    chunk: the longest chunk sets a launch's time) overlap the next passes'
+    chunking and digests.  Combined GiB/s of input bytes; not part of `value`."""
+    from plakar_amd import device as devmod
+    from plakar_amd import hashing
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    batches = [devmod.DeviceBatch(bufs, opts, final=True, device=dev.index) for _ in range(nstreams)]
+
+    def one(i):
+        s = streams[i % nstreams]
+        b = batches[i % nstreams]
+        b.launch(s)
+        cut_lists = [b.cuts[k] for k in range(b.n)]
+        with torch.cuda.stream(s):
+            hashing.chunk_digests_batch(bufs, cut_lists, [b.res[k] for k in range(b.n)], stream=s)
+    for i in range(nstreams):  # warm-up
+        one(i)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(passes):
+        one(i)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    total = sum(t.numel() for t in bufs) * passes
+    return dict(value=round(total / el / GIB, 2), unit="GiB/s", streams=nstreams, passes=passes,
+                ms_per_pass=round(el / passes * 1e3, 3),
+                bound="digest kernel occupancy: each pass's chunks in flight x the per-64-B-block latency of one "
+                      "SHA-256 chain (~1.9 us at one wave per SIMD); LDS (64 KiB per digest workgroup) caps "
+                      "concurrent passes")
+
+
 def cpu_baseline(bufs_host, cuts_dev, opts, seconds, threads=1):
     """The CPU oracle (scalar C restatement of the reference chunker, 1 thread)
     timed on a bounded sample of the same workload; also checks that the GPU
@@ -256,6 +291,8 @@ def main():
                          "own workspace, so one batch's resolution kernels overlap the next batch's scan")
     ap.add_argument("--digest-reps", type=int, default=3,
                     help="reps of the per-chunk SHA-256 + histogram leg (SURVEY.md 8f; 0 = skip)")
+    ap.add_argument("--digest-streams", type=int, default=4,
+                    help="passes in flight in the pipelined chunk + digest leg")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="reps of the PCIe-inclusive host-buffer leg (0 = skip)")
     args = ap.parse_args()
@@ -402,6 +439,8 @@ def main():
     digest = None
     if not host_mode and args.digest_reps > 0:
         digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0 and world == 1)
+        digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_streams,
+                                                                  max(args.digest_streams * 2, 8))
 
     baseline, parity, e2e = None, None, None
     if rank == 0 and world == 1:
