@@ -178,7 +178,11 @@ constexpr uint32_t kDbgTs = 16;
 constexpr uint32_t kDbgGraph = 32;  // with kDbgTs: k_resolve slots 5-7 time graph_build's phases
 constexpr uint32_t kTsScan = 0;                       // 4 per scan workgroup (<= 4096)
 constexpr uint32_t kTsRes = kTsScan + 4 * 4096;       // 8 per resolution segment (<= 16384)
-constexpr uint32_t kTsSlots = kTsRes + 8 * 16384;
+constexpr uint32_t kTsClk = kTsRes + 8 * 16384;     // clock ring (B.debug & kDbgClk): 4 per scan launch
+constexpr uint32_t kClkRecs = 4096;
+constexpr uint32_t kTsClkN = kTsClk + 4 * kClkRecs;   // ring counter
+constexpr uint32_t kTsSlots = kTsClkN + 1;
+constexpr uint32_t kDbgClk = 64;
 __device__ uint64_t g_ts[kTsSlots];
 
 __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
@@ -420,6 +424,13 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
         if (gt < 2) W.tick[gt] = 0u;
         if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
     }
+    // clock ring: workgroup 0's span in the 100-MHz and the shader-clock counters
+    uint32_t clk = 0;
+    if (!kMaskL && (B.debug & kDbgClk) && blockIdx.x == 0 && threadIdx.x == 0) {
+        clk = kTsClk + 4u * uint32_t(atomicAdd(reinterpret_cast<unsigned long long *>(&g_ts[kTsClkN]), 1ull) % kClkRecs);
+        g_ts[clk] = __builtin_amdgcn_s_memrealtime();
+        g_ts[clk + 1] = __builtin_amdgcn_s_memtime();
+    }
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, kMaskL ? P.fl_sh : P.fs_sh);
     __syncthreads();
     if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
@@ -585,6 +596,10 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
         if (lane == 0) W.validL[task] = 1u;
     }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
+    if (clk && threadIdx.x == 0) {
+        g_ts[clk + 2] = __builtin_amdgcn_s_memrealtime();
+        g_ts[clk + 3] = __builtin_amdgcn_s_memtime();
+    }
 }
 
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)

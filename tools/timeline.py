@@ -28,6 +28,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--bins", type=int, default=0, help="only print per-bin pass rates (bins of this many passes)")
     a = ap.parse_args()
     ks = load(a.csv)
     is_scan = lambda n: n.endswith("k_scan") or n.endswith("k_scan_f")  # noqa: E731
@@ -35,6 +36,18 @@ def main():
     npass = a.warmup + a.steps
     if len(starts) < npass:
         raise SystemExit(f"only {len(starts)} scans in the trace")
+    if a.bins:
+        t = [ks[i][0] for i in starts[:npass + 1]]
+        print("passes        us/pass   scan_us(avg)   resolve_us(avg)")
+        for b0 in range(0, npass, a.bins):
+            b1 = min(npass, b0 + a.bins)
+            if b1 >= len(t):
+                break
+            sc = [(ks[starts[p]][1] - ks[starts[p]][0]) / 1e3 for p in range(b0, b1)]
+            rs = [(e - s) / 1e3 for s, e, n in ks[starts[b0]:starts[b1]] if n.endswith("k_resolve")]
+            print(f"{b0:5d}-{b1 - 1:<5d} {(t[b1] - t[b0]) / 1e3 / (b1 - b0):9.1f} {sum(sc) / len(sc):12.1f} "
+                  f"{(sum(rs) / len(rs)) if rs else 0:14.1f}")
+        return
     print(f"{'pass':>4} {'t0_us':>10} {'scan_us':>8} {'gap_next_us':>11}  kernels (us)")
     per = defaultdict(list)
     for p in range(npass):
