@@ -267,13 +267,20 @@ int cdc_set_debug_mode(int mode);
 
 /* When and how the MaskL candidate index is built: 0 = never (walkers
  * raw-scan every MaskL region), 1 = adaptive (default: while recent launch
- * groups on the device needed it, in the same pass as the MaskS index
- * (k_scan_f), and on every 16th group as a probe by k_scan_l), 2 = every
- * launch group in the fused pass, 3 = every launch group by k_scan_l.  Cut points never depend on it; tests use it to cover every
- * path.  Initial value from the CDC_MASKL_INDEX environment variable.  Not a
+ * groups on the device needed it, in the same pass as the MaskS index where
+ * the masks admit it, else by k_scan_l; every 16th group otherwise runs the
+ * selection test alone as a probe), 2 = every launch group in the fused pass,
+ * 3 = every launch group by k_scan_l.  Cut points never depend on it; tests
+ * use it to cover every path.  Setting a mode clears the adaptive state.
+ * Initial value from the CDC_MASKL_INDEX environment variable.  Not a
  * reference interface (the Go chunker has no index).  Returns CDC_OK or
  * CDC_E_INVALID. */
 int cdc_set_maskl_index_mode(int mode);
+
+/* Adaptive MaskL state of one device (diagnostics, after a device sync):
+ * *hint = 1 while the next launch groups build the MaskL index (a recent
+ * group needed it), *groups = launch groups issued on the device so far.  Not a reference interface. */
+int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups);
 
 /* Live profiling of the device path: when enabled, every launch group records
  * hipEvents on its stream before/after the scan kernel and after the last

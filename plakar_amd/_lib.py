@@ -128,6 +128,7 @@ SIGNATURES = {
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_debug_maskl_state": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_uint32), _P(ctypes.c_uint64)]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),
                                            _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
@@ -146,6 +147,8 @@ def lib():
                 "(build it with `python -m plakar_amd.build`); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("PLAKAR_CDC_LIB") and not hasattr(L, name):
+                continue  # an older variant build (A/B runs) may lack newer entry points
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -61,8 +61,8 @@ struct DeviceCtx {
     uint64_t bounce_cap = 0;
     hipEvent_t bounce_ev[kBounces] = {nullptr, nullptr};
     int next_bounce = 0;
-    // Adaptive MaskL index (run_group): k_scan_l raises *hint_h (mapped host
-    // memory) whenever some scan task needed the index; groups launch k_scan_l
+    // Adaptive MaskL index (run_group): k_maskl_probe / k_scan_l raise *hint_h
+    // (mapped host memory) when some scan task needs the index; groups build it
     // while the hint is set, and every 16th group probes when it is not.
     uint32_t *hint_h = nullptr, *hint_d = nullptr;
     std::atomic<uint64_t> groups{0};
@@ -282,22 +282,24 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         return e ? uint32_t(atoi(e)) : 0u;
     }();
     B.debug = dbg;
-    // MaskL index (k_scan_l).  CDC_MASKL_INDEX: 0 off (walkers raw-scan every
-    // MaskL region), 1 adaptive (default), 2 every group.  Adaptive: launched
-    // while recent groups on this device needed it (the hint k_scan_l raises),
-    // otherwise on every 16th group as a probe; the hint decays every 1024
-    // groups.  Walkers use the index only in a group that built it, so cut
-    // points never depend on this choice.
+    // MaskL index.  CDC_MASKL_INDEX / cdc_set_maskl_index_mode: 0 off (walkers
+    // raw-scan every MaskL region), 1 adaptive (default), 2 every group (in the
+    // MaskS pass, k_scan_f, where the masks admit it), 3 every group by
+    // k_scan_l.  Adaptive: built while the hint is set (fused where the masks
+    // admit it, else k_scan_l, which re-raises it); otherwise every 16th group
+    // runs the selection test alone (k_maskl_probe: no LDS, so it does not wait
+    // for whole CUs beside the other stream's scan) and raises the hint; the
+    // hint decays every 1024 groups.  Walkers use the index only for tasks
+    // whose scan built it, so cut points never depend on this choice.
     const uint32_t mli = maskl_index_mode().load(std::memory_order_relaxed);
     {
         const uint64_t k = ctx->groups.fetch_add(1, std::memory_order_relaxed);
         volatile uint32_t *hint = ctx->hint_h;
         if (hint && k % 1024 == 1023) *hint = 0u;
         const bool hinted = !hint || *hint != 0u;
-        B.maskl_index = mli >= 2 || (mli == 1 && (k % 16 == 0 || hinted)) ? 1u : 0u;
-        // fused (k_scan_f: both indexes in one pass over the bytes) while the
-        // hint says the index is needed; the probes re-check with k_scan_l
+        B.maskl_index = mli >= 2 || (mli == 1 && hinted) ? 1u : 0u;
         B.maskl_fused = P.fm_ok && (mli == 2 || (mli == 1 && hinted)) ? 1u : 0u;
+        B.maskl_probe = mli == 1 && !hinted && k % 16 == 0 ? 1u : 0u;
         B.maskl_hint = ctx->hint_d;
     }
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
@@ -636,6 +638,23 @@ int cdc_set_maskl_index_mode(int mode)
 {
     if (mode < 0 || mode > 3) return CDC_E_INVALID;
     maskl_index_mode().store(uint32_t(mode), std::memory_order_relaxed);
+    // a new mode starts the adaptive state afresh (no recent MaskL request)
+    Global &g = G();
+    std::lock_guard<std::mutex> lock(g.mu);
+    for (DeviceCtx *c : g.devs)
+        if (c && c->hint_h) *static_cast<volatile uint32_t *>(c->hint_h) = 0u;
+    return CDC_OK;
+}
+
+int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups)
+{
+    if (!hint || !groups) return CDC_E_INVALID;
+    DeviceCtx *ctx = nullptr;
+    const int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    if (hipSetDevice(device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return CDC_E_DEVICE;
+    *hint = ctx->hint_h ? *static_cast<volatile uint32_t *>(ctx->hint_h) : 1u;
+    *groups = ctx->groups.load(std::memory_order_relaxed);
     return CDC_OK;
 }
 

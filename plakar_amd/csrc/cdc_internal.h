@@ -66,7 +66,8 @@ struct Batch {
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
     uint32_t maskl_index;    // 1: k_scan_l builds the MaskL index of long MaskS-free stretches (walkers use it)
     uint32_t maskl_fused;    // 1 (with maskl_index): k_scan_f builds both indexes of every task in one pass
-    uint32_t *maskl_hint;    // mapped host word: k_scan_l sets it when some task needed the MaskL index
+    uint32_t *maskl_hint;    // mapped host word: set when some task needed the MaskL index
+    uint32_t maskl_probe;    // 1: k_maskl_probe runs the selection test (adaptive mode, hint not set)
     uint64_t seg;            // resolution segment length in bytes
     BufDesc b[kMaxBufsPerLaunch];
 };

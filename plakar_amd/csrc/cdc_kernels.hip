@@ -181,7 +181,8 @@ constexpr uint32_t kTsRes = kTsScan + 4 * 4096;       // 8 per resolution segmen
 constexpr uint32_t kTsClk = kTsRes + 8 * 16384;     // clock ring (B.debug & kDbgClk): 4 per scan launch
 constexpr uint32_t kClkRecs = 4096;
 constexpr uint32_t kTsClkN = kTsClk + 4 * kClkRecs;   // ring counter
-constexpr uint32_t kTsSlots = kTsClkN + 1;
+constexpr uint32_t kTsHw = kTsClkN + 1;               // per scan workgroup: XCC_ID << 32 | HW_ID (kDbgTs)
+constexpr uint32_t kTsSlots = kTsHw + 4096;
 constexpr uint32_t kDbgClk = 64;
 __device__ uint64_t g_ts[kTsSlots];
 
@@ -433,7 +434,13 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     }
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, kMaskL ? P.fl_sh : P.fs_sh);
     __syncthreads();
-    if (!kMaskL && threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
+    if (!kMaskL && threadIdx.x == 0) {
+        dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
+        if (blockIdx.x < 4096)
+            dbg_ts(B, kTsHw + blockIdx.x,
+                   uint64_t(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11))) << 32 |
+                       uint32_t(__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11))));
+    }
     const char *tab = s_lds;
     if (task >= B.total_tasks || !act) return;
     uint32_t b = 0;
@@ -618,6 +625,26 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan_l(const Batch B, const D
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan_f(const Batch B, const DevParams P, const Workspace W)
 {
     scan_body<false, true>(B, P, W);
+}
+
+// The adaptive MaskL probe: the selection test of k_scan_l alone (one wave
+// per scan task, no LDS, so it runs beside other kernels), raising the hint
+// when some task would need the MaskL index.  The probing group itself builds
+// no index (its walkers raw-scan); the hint makes the next groups build it.
+constexpr uint32_t kProbeWaves = 4;
+
+__global__ __launch_bounds__(kProbeWaves * 64) void k_maskl_probe(const Batch B, const DevParams P, const Workspace W)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t task = blockIdx.x * kProbeWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (task >= B.total_tasks) return;
+    uint32_t b = 0;
+    while (b + 1 < B.nbufs && task >= B.b[b + 1].task_base) ++b;
+    const BufDesc &D = B.b[b];
+    const uint64_t t = task - D.task_base;
+    if (t * 64ull * B.scan_lane >= D.len) return;
+    if (maskl_needed(B, P, W, D, t, lane) && lane == 0 && B.maskl_hint)
+        __hip_atomic_store(B.maskl_hint, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // DPP helpers (in-row lane shifts, no LDS round trip; ds_bpermute-based
@@ -1937,6 +1964,9 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     // exit after one look at the MaskS index on ordinary data)
     if (B.total_tasks > 0 && B.maskl_index && !fused)
         hipLaunchKernelGGL(k_scan_l, sgrid, sblock, 0, st, B, P, W);
+    else if (B.total_tasks > 0 && B.maskl_probe)
+        hipLaunchKernelGGL(k_maskl_probe, dim3((B.total_tasks + kProbeWaves - 1) / kProbeWaves), dim3(kProbeWaves * 64),
+                           0, st, B, P, W);
     const dim3 rgrid(B.total_segs > 0 ? (B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG : 1u);
     if (prof)
         hipExtLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, nullptr, pr.e2, 0, B, P, W);

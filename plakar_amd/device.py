@@ -93,3 +93,12 @@ def set_maskl_index_mode(mode):
     launch group in the fused pass (k_scan_f), 3 = every launch group by
     k_scan_l. Cut points do not depend on it."""
     check(lib().cdc_set_maskl_index_mode(int(mode)))
+
+
+def maskl_state(device=0):
+    """Adaptive MaskL state (diagnostics): (1 while the next launch groups
+    build the MaskL index because a recent group asked for MaskL candidates,
+    else 0; launch groups issued on the device)."""
+    hint, groups = ctypes.c_uint32(), ctypes.c_uint64()
+    check(lib().cdc_debug_maskl_state(int(device), ctypes.byref(hint), ctypes.byref(groups)))
+    return hint.value, groups.value

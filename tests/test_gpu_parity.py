@@ -176,12 +176,37 @@ def test_maskl_index_modes(oracle, mode):
         assert_same(got, ref, f"maskl mode {mode} rep {rep}")
 
 
+def test_maskl_adaptive_follows_the_data(oracle):
+    """Adaptive mode: random data never raises the MaskL hint; on C3-like
+    data a probing group (every 16th) raises it and the next groups build the
+    MaskL index. Cuts are identical in every group."""
+    gear = _placeholder()
+    _lib.ensure_init(gear=gear)
+    device.set_maskl_index_mode(1)  # clears the adaptive state
+    assert device.maskl_state()[0] == 0
+    rnd = random_bytes(8 << 20, 73)
+    ref = oracle.chunk(rnd, gear, **DEF)
+    for rep in range(17):  # at least one probing group
+        (got,), _ = gpu_chunk([rnd], DEF, gear=gear)
+        assert_same(got, ref, f"random rep {rep}")
+    assert device.maskl_state()[0] == 0, "random data raised the MaskL hint"
+    low = low_entropy(24 << 20, 74)
+    ref = oracle.chunk(low, gear, **DEF)
+    assert (ref[:, 1] > DEF["normal_size"]).any()
+    built = 0
+    for rep in range(20):
+        (got,), _ = gpu_chunk([low], DEF, gear=gear)
+        assert_same(got, ref, f"low-entropy rep {rep}")
+        built += device.maskl_state()[0]
+    assert built >= 3, "the probe never raised the MaskL hint"
+
+
 @pytest.mark.parametrize("masks", [
     (0x0000000000001FFF, 0x00000000000001FF),  # MaskL inside MaskS's span: fused window exists
     (0x0000000000001FFF, 0x00000000000301FF),  # MaskL's top bit above MaskS's: no fused window
     (0x0003590703530000, 0x0000800000000001),  # MaskL spans 48 bits: no 32-bit window
 ], ids=["fusable", "maskl-above", "maskl-wide"])
-@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_maskl_index_alternative_masks(oracle, masks, mode):
     """The fused pass's MaskL window is derived from the masks; where none
     exists, mode 2 falls back to k_scan + k_scan_l. At these sizes many
@@ -195,7 +220,7 @@ def test_maskl_index_alternative_masks(oracle, masks, mode):
     ref = oracle.chunk(data, gear, mask_s=ms, mask_l=ml, **p)
     assert (ref[:, 1] > p["normal_size"]).any(), "no chunk reaches the MaskL region"
     t = torch.from_numpy(data).cuda()
-    for rep in range(2):
+    for rep in range(3):
         b = device.DeviceBatch([t], _opts(p))
         b.launch()
         (c,), _ = b.results()

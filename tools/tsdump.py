@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 K_SCAN, K_RES = 0, 4 * 4096
-K_SLOTS = K_RES + 8 * 16384
+K_HW = K_RES + 8 * 16384 + 4 * 4096 + 1
+K_SLOTS = K_HW + 4096
 
 
 def pct(a, qs=(0, 50, 90, 100)):
@@ -58,6 +59,26 @@ def main():
     print(f"scan WGs {len(scan)}: start {pct(us(scan[:, 0]))}")
     print(f"  fill done {pct(us(scan[:, 1]))}")
     print(f"  wave0 end {pct(us(scan[:, 2]))}")
+    print(f"  wave1 end {pct(us(scan[:, 3]))}   |wave0 - wave1| {pct(np.abs(scan[:, 2] - scan[:, 3]) / 100.0)}")
+    print(f"  duration (wave0 end - start) {pct((scan[:, 2] - scan[:, 0]) / 100.0)}")
+    hw = ts[K_HW:K_HW + len(scan)]
+    xcc = (hw >> 32) & 0xF
+    hwid = hw & 0xFFFFFFFF
+    cu = (hwid >> 8) & 0xF
+    se = (hwid >> 13) & 0x7
+    sh = (hwid >> 12) & 0x1
+    end = us(scan[:, 2])
+    for x in range(8):
+        sel = xcc == x
+        if sel.any():
+            print(f"    xcc {x}: {int(sel.sum())} WGs, end {pct(end[sel], (0, 50, 100))}")
+    for e in range(int(se.max()) + 1):
+        sel = se == e
+        if sel.any():
+            print(f"    se {e}: {int(sel.sum())} WGs, end {pct(end[sel], (0, 50, 100))}")
+    order = np.argsort(end)
+    print("  earliest WGs (blk xcc se sh cu end):", [(int(i), int(xcc[i]), int(se[i]), int(sh[i]), int(cu[i]), round(float(end[i]), 1)) for i in order[:6]])
+    print("  latest WGs:", [(int(i), int(xcc[i]), int(se[i]), int(sh[i]), int(cu[i]), round(float(end[i]), 1)) for i in order[-6:]])
     idx = np.nonzero(ts[K_SCAN:K_RES].reshape(-1, 4)[:, 0] > 0)[0]
     for x in range(8):  # blockIdx % 8 ~ XCD
         sel = (idx % 8) == x
