@@ -208,8 +208,9 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
 // the lane's run and lanes past the buffer's end need no separate code path:
 // every stage of every lane runs the same straight-line loop.
 //
-// The next group's 16 Gear gathers are issued a quarter at a time into the
-// registers the current group's roll has just consumed.
+// The next group's 16 Gear gathers are issued byte by byte between the links
+// of the current group's fingerprint chain, into the registers its roll has
+// just consumed.
 //
 // DMA addressing: one wave-uniform 64-bit base (SGPR pair) and one 32-bit
 // per-lane offset per piece, the base advanced per stage; a wave whose pieces
@@ -563,20 +564,25 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             uint32_t acc = 0xFFFFFFFFu, accL = 0xFFFFFFFFu;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
+                // byte by byte: the next group's address and gather between the
+                // links of the fingerprint chain (a dependent v_lshl_add_u64
+                // waits ~9 cycles, an independent one issues every ~5)
 #pragma unroll
                 for (int k = 4 * q; k < 4 * q + 4; k += 2) {
+                    const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
                     fp = (fp << 1) + cg[k];
+                    ng[k] = lds_gear(tab, a0);
                     const uint32_t k0 = uint32_t(fp >> 32) & vhi;
                     uint32_t l0 = 0;
                     if constexpr (kFused) l0 = __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm;
+                    const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
                     fp = (fp << 1) + cg[k + 1];
+                    ng[k + 1] = lds_gear(tab, a1);
                     acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
                     if constexpr (kFused)
                         accL = umin3(accL, l0, __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int k = 4 * q; k < 4 * q + 4; ++k) ng[k] = lds_gear(tab, gear_addr(laneoff, word_of(nx, k >> 2), k));
                 __builtin_amdgcn_sched_barrier(0);
                 if (q == 1 && gi + 1 == kGroups && t + 2 < TT) {
                     asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the row reads precede these 8 gathers

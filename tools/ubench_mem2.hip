@@ -9,6 +9,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
+
+#include <vector>
 
 __device__ __forceinline__ void glds_s(uint32_t off, const void *base, uint32_t lds)
 {
@@ -90,13 +93,44 @@ void run(const uint8_t *buf, uint32_t *out, uint64_t runlen, int wgs)
     fflush(stdout);
 }
 
-int main()
+// Cold start: every launch of the first N timed on its own (the clock ramp).
+template <int CHUNK, int DEPTH, int WAVES>
+void cold(const uint8_t *buf, uint32_t *out, uint64_t runlen, int wgs, int n)
+{
+    std::vector<hipEvent_t> ev(n + 1);
+    for (auto &e : ev) (void)hipEventCreate(&e);
+    (void)hipEventRecord(ev[0]);
+    for (int i = 0; i < n; ++i) {
+        hipLaunchKernelGGL((kern<CHUNK, DEPTH, WAVES>), dim3(wgs), dim3(WAVES * 64), 0, 0, buf, runlen, out);
+        (void)hipEventRecord(ev[i + 1]);
+    }
+    (void)hipDeviceSynchronize();
+    const double bytes = double(wgs) * WAVES * 64 * double(runlen / CHUNK * CHUNK);
+    double t = 0;
+    for (int b = 0; b < n; b += 10) {
+        double sum = 0;
+        for (int i = b; i < b + 10 && i < n; ++i) {
+            float ms;
+            (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+            sum += ms;
+        }
+        printf("launches %3d-%3d  t=%7.2f ms  avg %6.1f us  %7.1f GB/s\n", b, b + 9, t, sum / 10 * 1e3,
+               bytes / (sum / 10 * 1e-3) / 1e9);
+        t += sum;
+    }
+}
+
+int main(int argc, char **argv)
 {
     uint8_t *buf;
     uint32_t *out;
     (void)hipMalloc(&buf, (1ull << 30) + (4 << 20));
     (void)hipMalloc(&out, 64);
     (void)hipMemset(buf, 1, (1ull << 30) + (4 << 20));
+    if (argc > 1 && strcmp(argv[1], "cold") == 0) {
+        cold<128, 1, 12>(buf, out, 5632, 248, 300);
+        return 0;
+    }
     // one GiB: wgs * waves * 64 * run
     run<128, 1, 12>(buf, out, 5632, 248);
     run<128, 2, 12>(buf, out, 5632, 248);
