@@ -128,6 +128,22 @@ void cdc_default_opts(cdc_opts *out);
 int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out,
               uint64_t out_cap, uint64_t *out_counts, uint64_t *out_needed);
 
+/* ---- collector: concurrent per-file callers -> device batches -------------------
+ * plakar chunks each file in its own goroutine (snapshot/backup.go:216-225,
+ * each running the Next() loop of backup.go:647-665).  A collector takes such
+ * per-file calls from any number of threads and submits them to the devices
+ * as batches: a batch closes at batch_bytes (0: 256 MiB), at 64 files, or
+ * max_wait_us after its first file arrived; each batch is one cdc_chunk.
+ * cdc_collector_chunk blocks until the caller's own cut list is back and has
+ * cdc_chunk's contract for one buffer (CDC_E_NOSPACE with *count set when cap
+ * is too small).  cdc_collector_free drains pending calls, then stops. */
+typedef struct cdc_collector cdc_collector;
+int cdc_collector_new(const cdc_opts *opts, uint64_t batch_bytes, uint32_t max_wait_us, cdc_collector **out);
+int cdc_collector_chunk(cdc_collector *c, const void *data, uint64_t len, cdc_cut *out, uint64_t cap,
+                        uint64_t *count);
+int cdc_collector_stats(cdc_collector *c, uint64_t *requests, uint64_t *batches);
+void cdc_collector_free(cdc_collector *c);
+
 /* ---- packfile builder: the consumer of the cut lists ---------------------------
  * snapshot/packer.go + packfile/packfile.go: blobs are appended to a
  * packfile whose bytes are those of (*PackFile).Serialize (packfile.go:241-294):

@@ -125,6 +125,11 @@ SIGNATURES = {
                                                  ctypes.c_uint64, _P(ctypes.c_uint64)]),
     "cdc_packer_reset": (None, [ctypes.c_void_p]),
     "cdc_packer_free": (None, [ctypes.c_void_p]),
+    "cdc_collector_new": (ctypes.c_int, [_P(cdc_opts), ctypes.c_uint64, ctypes.c_uint32, _P(ctypes.c_void_p)]),
+    "cdc_collector_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, _P(cdc_cut),
+                                           ctypes.c_uint64, _P(ctypes.c_uint64)]),
+    "cdc_collector_stats": (ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
+    "cdc_collector_free": (None, [ctypes.c_void_p]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),

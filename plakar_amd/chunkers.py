@@ -256,3 +256,52 @@ class FileBatch:
             self.close()
         except Exception:
             pass
+
+
+class Collector:
+    """Concurrent per-file chunking, batched for the device (cdc_collector_*).
+
+    plakar chunks each file in its own goroutine (snapshot/backup.go:216-225,
+    each running the Next() loop of backup.go:647-665).  Threads call
+    `chunk(buf)` concurrently; the library queues the calls and submits them
+    to the devices as batches (up to `batch_bytes`, 64 files, or `max_wait_us`
+    after the first file of a batch arrived).  Each call blocks until its own
+    cut list is back: a uint64 (n, 2) array of (offset, length) rows."""
+
+    def __init__(self, opts, batch_bytes=256 << 20, max_wait_us=200):
+        ensure_init()
+        self._opts = opts
+        o = opts._c()
+        self._h = ctypes.c_void_p()
+        check(lib().cdc_collector_new(ctypes.byref(o), int(batch_bytes), int(max_wait_us), ctypes.byref(self._h)),
+              "cdc_collector_new")
+
+    def chunk(self, buf):
+        import numpy as np
+        a = np.ascontiguousarray(np.asarray(buf, dtype=np.uint8).reshape(-1))
+        cap = a.size // max(self._opts.MinSize, 1) + 2
+        out = np.zeros((cap, 2), dtype=np.uint64)
+        n = ctypes.c_uint64()
+        check(lib().cdc_collector_chunk(self._h, ctypes.c_void_p(a.ctypes.data if a.size else 0), a.size,
+                                        ctypes.cast(out.ctypes.data, ctypes.POINTER(_lib.cdc_cut)), cap,
+                                        ctypes.byref(n)), "Collector.chunk")
+        res = out[:n.value].copy()
+        res[:, 1] &= np.uint64(0xFFFFFFFF)
+        return res
+
+    def stats(self):
+        """(requests, batches) so far."""
+        r, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().cdc_collector_stats(self._h, ctypes.byref(r), ctypes.byref(b)))
+        return r.value, b.value
+
+    def close(self):
+        if self._h:
+            lib().cdc_collector_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

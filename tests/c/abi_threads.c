@@ -11,6 +11,8 @@
  *      scanner goroutines of snapshot/backup.go:216-225 calling in parallel.
  *   3. cdc_batch_add_files: files read by the library into its pinned arena,
  *      then one cdc_batch_chunk (the importer, snapshot/importer/fs/fs.go:69-71).
+ *   4. cdc_collector_chunk from 8 threads: per-file calls batched for the
+ *      device (the scanner fan-out of snapshot/backup.go:216-225).
  *
  * Every result is compared with the oracle; exit status 0 = all identical.
  */
@@ -199,6 +201,58 @@ static int test_threads(void)
     return bad;
 }
 
+/* ---- 4. collector: per-file calls from 8 threads, batched ------------------- */
+static cdc_collector *g_col;
+
+static void *collector_main(void *arg)
+{
+    job *j = arg;
+    for (int i = 0; i < 4 && !j->bad; ++i) {
+        const uint64_t n = ((uint64_t)(j->id * 4 + i) * 104729u % 23u) << 20 | (uint64_t)(j->id * 977 + i);
+        uint8_t *p = malloc(n + 1);
+        fill(p, n, 3000 + (uint64_t)(j->id * 4 + i));
+        const uint64_t cap = n / g_opts.min_size + 2;
+        cdc_cut *out = malloc(cap * sizeof(cdc_cut));
+        uint64_t cnt = 0, *roff;
+        uint32_t *rlen;
+        const int st = cdc_collector_chunk(g_col, p, n, out, cap, &cnt);
+        const uint64_t nref = ref_cuts(p, n, &roff, &rlen);
+        j->bad |= st != CDC_OK || cnt != nref;
+        for (uint64_t q = 0; q < nref && !j->bad; ++q) j->bad |= out[q].offset != roff[q] || out[q].length != rlen[q];
+        if (j->bad) fprintf(stderr, "collector thread %d file %d differs (status %d)\n", j->id, i, st);
+        j->chunks += cnt;
+        free(out);
+        free(roff);
+        free(rlen);
+        free(p);
+    }
+    return NULL;
+}
+
+static int test_collector(void)
+{
+    if (cdc_collector_new(&g_opts, 32u << 20, 2000, &g_col) != CDC_OK) return 1;
+    pthread_t th[kThreads];
+    job jobs[kThreads];
+    for (int t = 0; t < kThreads; ++t) {
+        jobs[t] = (job){t, 0, 0};
+        pthread_create(&th[t], NULL, collector_main, &jobs[t]);
+    }
+    int bad = 0;
+    uint64_t chunks = 0, req = 0, batches = 0;
+    for (int t = 0; t < kThreads; ++t) {
+        pthread_join(th[t], NULL);
+        bad |= jobs[t].bad;
+        chunks += jobs[t].chunks;
+    }
+    cdc_collector_stats(g_col, &req, &batches);
+    cdc_collector_free(g_col);
+    bad |= req != kThreads * 4 || batches >= req;
+    printf("collector: %llu files from %d threads in %llu batches, %llu chunks %s\n", (unsigned long long)req, kThreads,
+           (unsigned long long)batches, (unsigned long long)chunks, bad ? "MISMATCH" : "identical");
+    return bad;
+}
+
 /* ---- 3. pinned file arena -------------------------------------------------- */
 static int test_files(void)
 {
@@ -272,6 +326,7 @@ int main(void)
     int bad = test_read_callback();
     bad |= test_threads();
     bad |= test_files();
+    bad |= test_collector();
     /* re-init with the same device set is accepted; another set is refused */
     bad |= cdc_init(0, NULL, 0, 0, 0) != CDC_OK;
     bad |= cdc_init(1u << 31, NULL, 0, 0, 0) != CDC_E_NO_DEVICE && cdc_device_count() < 32;

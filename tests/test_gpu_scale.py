@@ -188,3 +188,37 @@ def test_backup_batch_packfiles(oracle):
         assert set(got) == set(want) - {first}
         for c, blob in got.items():
             assert blob == (want[c] if encode is None else zlib.compress(want[c], 1))
+
+
+def test_collector_concurrent_callers(oracle):
+    """Per-file calls from 16 threads at once through one collector (the
+    scanner goroutines of snapshot/backup.go:216-225, each chunking its own
+    file): every cut list matches the oracle, and the calls were batched."""
+    import threading
+    _lib.ensure_init()
+    gear = _lib.default_gear()
+    rng = np.random.default_rng(5)
+    sizes = [int(x) for x in rng.choice([0, 1, 4096, 65536, 70000, 1 << 20, 3 << 20, 9 << 20, 17 << 20], size=96)]
+    files = [random_bytes(n, 1200 + i) for i, n in enumerate(sizes)]
+    col = chunkers.Collector(OPTS, batch_bytes=64 << 20, max_wait_us=2000)
+    got = [None] * len(files)
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(t, len(files), 16):
+                got[i] = col.chunk(files[i])
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    for i, a in enumerate(files):
+        assert_same(got[i], oracle.chunk(a, gear, **DEF) if a.size else np.zeros((0, 2), np.uint64), f"file {i}")
+    req, batches = col.stats()
+    col.close()
+    assert req == len(files) and batches < req, (req, batches)
