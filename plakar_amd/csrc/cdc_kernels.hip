@@ -1846,10 +1846,12 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     seg = (seg + 15) & ~15ull;
     plan->seg = seg;
     // Scan lane length: one scan workgroup per CU (a workgroup holds 112 KiB of
-    // LDS), for a grid of CUs - 8 workgroups: measured on MI355X (1 GiB, lane
-    // lengths 4-8 KiB in 128-B steps), grids of 249 and fewer run at full HBM
-    // rate while 255 workgroups ran 30 % slower per workgroup although all of
-    // them were resident from the start; lane lengths are multiples of 256 B.
+    // LDS), for a target grid of one workgroup per CU; lane lengths are
+    // multiples of 256 B (odd multiples of 128 B ran slower), so 1 GiB takes
+    // 249 workgroups of 5,632-B lanes.  Against CUs - 8 (238 workgroups) that
+    // is +2.8 % pipelined from a cold start and +1 % for the isolated scan
+    // warm, but -1.3 % pipelined warm (fewer CUs left beside the scan for the
+    // previous pass's resolution).
     uint64_t total = 0;
     for (int i = 0; i < nbufs; ++i) total += lens[i];
     static const uint64_t cus = [] {
@@ -1859,7 +1861,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
             n = 256;
         return uint64_t(n);
     }();
-    uint64_t wgs = cus > 16 ? cus - 8 : cus;
+    uint64_t wgs = cus;
     if (const char *env = getenv("CDC_SCAN_WGS")) {
         const long v = atol(env);
         if (v >= 1 && v <= 65536) wgs = uint64_t(v);
