@@ -144,6 +144,30 @@ int cdc_collector_chunk(cdc_collector *c, const void *data, uint64_t len, cdc_cu
 int cdc_collector_stats(cdc_collector *c, uint64_t *requests, uint64_t *batches);
 void cdc_collector_free(cdc_collector *c);
 
+/* ---- Encode: LZ4 frame, then the AES-256-GCM stream ----------------------------
+ * (*Repository).Encode (repository/repository.go:212-236) of n blobs that sit
+ * in device memory at d_base + offsets[i], lens[i] bytes each:
+ *   compress != 0: the LZ4 frame of compression.DeflateLZ4Stream
+ *     (compression/compression.go:94-106; pierrec/lz4/v4 writer defaults:
+ *     4-MiB independent blocks, content checksum; a block that does not
+ *     shrink is stored);
+ *   key != NULL (32 bytes, host memory): then encryption.EncryptStream
+ *     (encryption/symmetric.go:72-163): subkey nonce (12) || Seal(key,
+ *     subkey nonce, subkey) (48) || per 64-KiB piece k of the stream: nonce
+ *     (12) || Seal(subkey, nonce, piece).  random (host, 56 bytes per blob:
+ *     subkey 32, subkey nonce 12, data nonce 12) supplies what crypto/rand
+ *     supplies in the reference; piece k's nonce is the data nonce with its
+ *     last four bytes XOR k (big-endian).
+ * Blob i's encoding lands at d_out + out_offsets[i] (device memory; host
+ * array of n + 1 offsets, out_offsets[n] = total).  Returns CDC_E_NOSPACE
+ * when out_cap is smaller than out_offsets[n].  Synchronous on `stream`. */
+int cdc_encode_device(int device, const void *d_base, const uint64_t *offsets, const uint64_t *lens, uint32_t n,
+                      int compress, const uint8_t *key, const uint8_t *random, uint8_t *d_out, uint64_t out_cap,
+                      uint64_t *out_offsets, void *stream);
+
+/* Upper bound of one blob's encoding (for out_cap). */
+uint64_t cdc_encode_bound(uint64_t len, int compress, int encrypt);
+
 /* ---- packfile builder: the consumer of the cut lists ---------------------------
  * snapshot/packer.go + packfile/packfile.go: blobs are appended to a
  * packfile whose bytes are those of (*PackFile).Serialize (packfile.go:241-294):

@@ -130,6 +130,10 @@ SIGNATURES = {
                                            ctypes.c_uint64, _P(ctypes.c_uint64)]),
     "cdc_collector_stats": (ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
     "cdc_collector_free": (None, [ctypes.c_void_p]),
+    "cdc_encode_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, _P(ctypes.c_uint64), _P(ctypes.c_uint64),
+                                         ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                         ctypes.c_void_p, ctypes.c_uint64, _P(ctypes.c_uint64), ctypes.c_void_p]),
+    "cdc_encode_bound": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int]),
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
@@ -150,6 +154,14 @@ def lib():
             raise ImportError(
                 f"libplakar_cdc.so not found at {LIB_PATH}: the HIP extension is required "
                 "(build it with `python -m plakar_amd.build`); there is no CPU fallback")
+        # With PyTorch in the process there are two HIP runtimes (torch's bundled
+        # one and the system's, which this library links); torch's must come up
+        # first, or torch then finds no device.
+        try:
+            import torch
+            torch.cuda.is_available()
+        except Exception:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             if os.environ.get("PLAKAR_CDC_LIB") and not hasattr(L, name):

@@ -1,0 +1,1059 @@
+// Encode on the device: plakar's (*Repository).Encode
+// (repository/repository.go:212-236) of a batch of blobs: the LZ4 frame of
+// compression.DeflateLZ4Stream (compression/compression.go:94-106,
+// github.com/pierrec/lz4/v4 v4.1.18 NewWriter defaults: independent blocks of
+// at most 4 MiB, content checksum on), then the AES-256-GCM stream of
+// encryption.EncryptStream (encryption/symmetric.go:72-163): a random subkey
+// sealed under the repository key, then every 64-KiB piece of the
+// compressed stream sealed under the subkey with its own nonce.
+//
+// Kernels, in launch order (one batch = the blobs of one call):
+//   k_xxh32       one wave per blob: XXH32 of the blob (the frame's content
+//                 checksum), its four accumulators on lanes 0-3
+//   k_lz4_seq     one wave per 16-KiB segment: greedy LZ4 match search over a
+//                 64-position window per step (hash table of 4,096 u16 in LDS,
+//                 matches found by ballot, extended 64 bytes per step);
+//                 sequences out as (match start, offset, length) records
+//   k_lz4_size    one workgroup per 4-MiB LZ4 block: literal runs across
+//                 segment boundaries, encoded size (raw when not smaller)
+//   k_enc_plan    one workgroup: frame sizes, block offsets in the frame,
+//                 GCM pieces and output offsets of every blob
+//   k_lz4_emit    one workgroup per block: the block's bytes in the frame
+//   k_frame_fin   one wave per blob: frame header, end mark, checksum
+//   k_blob_keys   one lane per blob: the subkey's round keys, H and its
+//                 powers H^1..H^64, and the sealed subkey (header)
+//   k_gcm         one wave per 64-KiB piece: AES-256-CTR (T-table in LDS)
+//                 and GHASH (4-bit tables: lane l hashes blocks l, l+64, ...
+//                 by Horner in H^64, then multiplies by its own H^e), tag
+//
+// Matches stay inside their 16-KiB segment, so compression ratios are those
+// of LZ4 with a 16-KiB window; any LZ4 decoder reads the frames (the tests
+// decode them with the system's liblz4).  Nonces and subkeys come from the
+// caller (the host fills them from the OS CSPRNG), as crypto/rand does in
+// the reference; piece k of a blob uses the blob's data nonce with its last
+// four bytes XOR k (big-endian), unique per subkey.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "cdc_internal.h"
+
+namespace enc {
+
+constexpr uint32_t kSegLZ = 16384;            // LZ4 match-search segment
+constexpr uint64_t kBlockLZ = 4ull << 20;     // LZ4 block (pierrec Block4Mb)
+constexpr uint32_t kPiece = 65536;            // EncryptStream chunkSize
+constexpr uint32_t kHashBits = 12;
+constexpr uint32_t kRecCap = kSegLZ / 4 + 2;  // records per segment (a match per 4 bytes at most)
+
+// ---------------------------------------------------------------------------
+// AES tables, built on the host (FIPS-197: S-box = affine(inverse in GF(2^8))).
+// ---------------------------------------------------------------------------
+__device__ uint32_t g_te0[256];
+__device__ uint8_t g_sbox[256];
+
+static void build_tables(uint32_t te0[256], uint8_t sbox[256])
+{
+    auto mul = [](uint8_t a, uint8_t b) {
+        uint8_t p = 0;
+        for (int i = 0; i < 8; ++i) {
+            if (b & 1) p ^= a;
+            const uint8_t hi = a & 0x80;
+            a = uint8_t(a << 1);
+            if (hi) a ^= 0x1B;
+            b >>= 1;
+        }
+        return p;
+    };
+    for (int x = 0; x < 256; ++x) {
+        uint8_t inv = 0;
+        if (x)
+            for (int y = 1; y < 256; ++y)
+                if (mul(uint8_t(x), uint8_t(y)) == 1) {
+                    inv = uint8_t(y);
+                    break;
+                }
+        uint8_t s = inv;
+        for (int i = 1; i <= 4; ++i) s ^= uint8_t((inv << i) | (inv >> (8 - i)));
+        sbox[x] = uint8_t(s ^ 0x63);
+    }
+    for (int x = 0; x < 256; ++x) {
+        const uint8_t s = sbox[x];
+        te0[x] = uint32_t(mul(s, 2)) << 24 | uint32_t(s) << 16 | uint32_t(s) << 8 | mul(s, 3);
+    }
+}
+
+__device__ __forceinline__ uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+__device__ __forceinline__ uint32_t rol32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// AES-256 key schedule (FIPS-197 §5.2), words big-endian.
+__device__ void aes256_expand(const uint8_t key[32], uint32_t rk[60], const uint8_t *sbox)
+{
+    for (int i = 0; i < 8; ++i)
+        rk[i] = uint32_t(key[4 * i]) << 24 | uint32_t(key[4 * i + 1]) << 16 | uint32_t(key[4 * i + 2]) << 8 |
+                key[4 * i + 3];
+    uint32_t rcon = 1;
+    for (int i = 8; i < 60; ++i) {
+        uint32_t t = rk[i - 1];
+        if (i % 8 == 0) {
+            t = rol32(t, 8);
+            t = uint32_t(sbox[t >> 24]) << 24 | uint32_t(sbox[(t >> 16) & 255]) << 16 |
+                uint32_t(sbox[(t >> 8) & 255]) << 8 | sbox[t & 255];
+            t ^= rcon << 24;
+            rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x1B : 0);
+        } else if (i % 8 == 4) {
+            t = uint32_t(sbox[t >> 24]) << 24 | uint32_t(sbox[(t >> 16) & 255]) << 16 |
+                uint32_t(sbox[(t >> 8) & 255]) << 8 | sbox[t & 255];
+        }
+        rk[i] = rk[i - 8] ^ t;
+    }
+}
+
+// One block, words big-endian (T-table form; Te1..3 are rotations of Te0).
+__device__ __forceinline__ void aes256_block(const uint32_t *rk, const uint32_t *te, const uint8_t *sb, uint32_t s[4])
+{
+    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t t0 = te[s0 >> 24] ^ ror32(te[(s1 >> 16) & 255], 8) ^ ror32(te[(s2 >> 8) & 255], 16) ^
+                            ror32(te[s3 & 255], 24) ^ rk[4 * r];
+        const uint32_t t1 = te[s1 >> 24] ^ ror32(te[(s2 >> 16) & 255], 8) ^ ror32(te[(s3 >> 8) & 255], 16) ^
+                            ror32(te[s0 & 255], 24) ^ rk[4 * r + 1];
+        const uint32_t t2 = te[s2 >> 24] ^ ror32(te[(s3 >> 16) & 255], 8) ^ ror32(te[(s0 >> 8) & 255], 16) ^
+                            ror32(te[s1 & 255], 24) ^ rk[4 * r + 2];
+        const uint32_t t3 = te[s3 >> 24] ^ ror32(te[(s0 >> 16) & 255], 8) ^ ror32(te[(s1 >> 8) & 255], 16) ^
+                            ror32(te[s2 & 255], 24) ^ rk[4 * r + 3];
+        s0 = t0;
+        s1 = t1;
+        s2 = t2;
+        s3 = t3;
+    }
+    s[0] = (uint32_t(sb[s0 >> 24]) << 24 | uint32_t(sb[(s1 >> 16) & 255]) << 16 | uint32_t(sb[(s2 >> 8) & 255]) << 8 |
+            sb[s3 & 255]) ^ rk[56];
+    s[1] = (uint32_t(sb[s1 >> 24]) << 24 | uint32_t(sb[(s2 >> 16) & 255]) << 16 | uint32_t(sb[(s3 >> 8) & 255]) << 8 |
+            sb[s0 & 255]) ^ rk[57];
+    s[2] = (uint32_t(sb[s2 >> 24]) << 24 | uint32_t(sb[(s3 >> 16) & 255]) << 16 | uint32_t(sb[(s0 >> 8) & 255]) << 8 |
+            sb[s1 & 255]) ^ rk[58];
+    s[3] = (uint32_t(sb[s3 >> 24]) << 24 | uint32_t(sb[(s0 >> 16) & 255]) << 16 | uint32_t(sb[(s1 >> 8) & 255]) << 8 |
+            sb[s2 & 255]) ^ rk[59];
+}
+
+// ---------------------------------------------------------------------------
+// GF(2^128) in GCM's bit order (SP 800-38D §6.3): an element is (hi, lo) =
+// the big-endian halves of its 16 bytes.  4-bit tables: T[i] = i * V for the
+// 4-bit value i read MSB-first (T[8] = V, T[4] = V x, ...).
+// ---------------------------------------------------------------------------
+struct G128 {
+    uint64_t hi, lo;
+};
+
+__device__ __forceinline__ G128 gx(G128 a, G128 b) { return {a.hi ^ b.hi, a.lo ^ b.lo}; }
+
+__device__ void gtable(G128 v, G128 t[16])
+{
+    auto half = [](G128 x) {  // x * x^1 (one right shift with reduction)
+        const uint64_t r = (x.lo & 1) ? 0xE100000000000000ull : 0;
+        return G128{(x.hi >> 1) ^ r, (x.lo >> 1) | (x.hi << 63)};
+    };
+    t[0] = {0, 0};
+    t[8] = v;
+    t[4] = half(t[8]);
+    t[2] = half(t[4]);
+    t[1] = half(t[2]);
+    for (int i = 3; i < 16; ++i)
+        if (i & (i - 1)) t[i] = gx(t[i & -i], t[i & (i - 1)]);
+}
+
+// rem_4bit[r]: the reduction of the 4 bits shifted out, in the top 16 bits.
+__device__ __forceinline__ uint64_t rem4(uint32_t r)
+{
+    uint64_t x = 0;
+    if (r & 1) x ^= 0x1C20;
+    if (r & 2) x ^= 0x3840;
+    if (r & 4) x ^= 0x7080;
+    if (r & 8) x ^= 0xE100;
+    return x << 48;
+}
+
+// x * V with V's 4-bit table (processed nibble by nibble from the last byte).
+template <typename TAB>
+__device__ __forceinline__ G128 gmul4(G128 x, const TAB &t)
+{
+    G128 z = {0, 0};
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+        const uint64_t w = i >= 16 ? x.lo : x.hi;
+        const uint32_t nib = uint32_t(w >> (4 * ((31 - i) & 15))) & 15;
+        if (i != 31) {
+            const uint32_t rem = uint32_t(z.lo) & 15;
+            z.lo = (z.hi << 60) | (z.lo >> 4);
+            z.hi = (z.hi >> 4) ^ rem4(rem);
+        }
+        const G128 e = t[nib];
+        z.hi ^= e.hi;
+        z.lo ^= e.lo;
+    }
+    return z;
+}
+
+// a * b bit by bit (SP 800-38D Algorithm 1), for a per-lane multiplier.
+__device__ G128 gmul_bits(G128 a, G128 b)
+{
+    G128 z = {0, 0}, v = b;
+    for (int i = 0; i < 128; ++i) {
+        const uint64_t bit = i < 64 ? (a.hi >> (63 - i)) & 1 : (a.lo >> (127 - i)) & 1;
+        if (bit) z = gx(z, v);
+        const uint64_t r = (v.lo & 1) ? 0xE100000000000000ull : 0;
+        v.lo = (v.lo >> 1) | (v.hi << 63);
+        v.hi = (v.hi >> 1) ^ r;
+    }
+    return z;
+}
+
+__device__ __forceinline__ G128 g_from_words(const uint32_t w[4])
+{
+    return {uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]};
+}
+
+// Per-blob GCM state (workspace): AES round keys of the subkey, the 4-bit
+// tables of H and H^64, and H^1..H^64.
+struct BlobKey {
+    uint32_t rk[60];
+    uint32_t pad[4];
+    G128 th[16];
+    G128 th64[16];
+    G128 hpow[64];
+};
+
+struct Seg {             // a 16-KiB LZ4 search segment
+    uint64_t src;        // byte offset in the input base
+    uint32_t len;
+    uint32_t rem;        // bytes from the segment's start to its LZ4 block's end
+};
+
+struct Blk {             // a 4-MiB LZ4 block
+    uint64_t src;
+    uint32_t len, blob;
+    uint32_t seg0, nseg;
+    uint32_t k;          // block index in its blob
+    uint32_t pad;
+};
+
+struct BlobDesc {
+    uint64_t src;        // byte offset in the input base
+    uint64_t len;
+    uint64_t slot;       // frame slot in the frame buffer (16-B aligned)
+    uint32_t blk0, nblk;
+};
+
+struct Batch {
+    const uint8_t *base;
+    uint32_t nblobs, nsegs, nblks, npieces_max;
+    uint32_t compress, encrypt;
+    const BlobDesc *blobs;
+    const Seg *segs;
+    const Blk *blks;
+    const uint8_t *rnd;       // per blob: subkey 32, subkey nonce 12, data nonce 12
+    const uint8_t *key;       // repository key (32 B, device)
+    uint8_t *frames;          // frame buffer
+    uint8_t *out;
+    uint64_t out_cap;
+    // workspace
+    uint2 *recs;              // kRecCap per segment
+    uint32_t *nrec;           // per segment
+    uint32_t *trail;          // per segment: literals after its last match (from its start when none)
+    uint32_t *blk_size;       // per block: encoded size, bit 31 = stored raw
+    uint64_t *blk_foff;       // per block: offset of its header in the frame
+    uint32_t *xxh;            // per blob
+    uint64_t *frame_len;      // per blob
+    uint64_t *out_off;        // nblobs + 1
+    uint32_t *piece_base;     // nblobs + 1
+    BlobKey *keys;            // per blob
+    uint64_t *status;         // [0]: CDC_E_NOSPACE when out_cap is too small
+};
+
+constexpr uint32_t kNoneU32 = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t ld32u(const uint8_t *p)  // unaligned
+{
+    return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+
+// ---------------------------------------------------------------------------
+// XXH32 (the frame's content checksum): lanes 0-3 run accumulators v1..v4 over
+// the 16-byte stripes, lane 0 the tail.
+// ---------------------------------------------------------------------------
+constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u, P5 = 374761393u;
+
+__global__ __launch_bounds__(256) void k_xxh32(const Batch B)
+{
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    if (w >= B.nblobs) return;
+    const BlobDesc D = B.blobs[w];
+    const uint8_t *p = B.base + D.src;
+    const uint64_t n = D.len, stripes = n / 16;
+    uint32_t v = 0;
+    if (lane < 4) {
+        v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0u : 0u - P1;
+        uint64_t s = 0;
+        for (; s + 8 <= stripes; s += 8) {
+            uint32_t in[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) in[j] = ld32u(p + 16 * (s + j) + 4 * lane);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v = rol32(v + in[j] * P2, 13) * P1;
+        }
+        for (; s < stripes; ++s) v = rol32(v + ld32u(p + 16 * s + 4 * lane) * P2, 13) * P1;
+    }
+    const uint32_t v1 = __shfl(v, 0), v2 = __shfl(v, 1), v3 = __shfl(v, 2), v4 = __shfl(v, 3);
+    if (lane != 0) return;
+    uint32_t h = n >= 16 ? rol32(v1, 1) + rol32(v2, 7) + rol32(v3, 12) + rol32(v4, 18) : P5;
+    h += uint32_t(n);
+    uint64_t i = stripes * 16;
+    for (; i + 4 <= n; i += 4) h = rol32(h + ld32u(p + i) * P3, 17) * P4;
+    for (; i < n; ++i) h = rol32(h + p[i] * P5, 11) * P1;
+    h ^= h >> 15;
+    h *= P2;
+    h ^= h >> 13;
+    h *= P3;
+    h ^= h >> 16;
+    B.xxh[w] = h;
+}
+
+// ---------------------------------------------------------------------------
+// k_lz4_seq: one wave per segment.  Record = (match start | offset << 16,
+// match length), segment-relative; the literals before a match are the bytes
+// since the previous match's end.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSeqWaves = 4;
+
+struct SeqLds {
+    uint32_t data[kSegLZ / 4 + 4];
+    uint16_t tab[1u << kHashBits];
+};
+
+__device__ __forceinline__ uint32_t lds_rd32(const SeqLds &L, uint32_t p)  // bytes p..p+3 (any p)
+{
+    const uint32_t w0 = L.data[p >> 2], w1 = L.data[(p >> 2) + 1];
+    return __builtin_amdgcn_alignbit(w1, w0, (p & 3u) * 8u);
+}
+
+__device__ __forceinline__ uint32_t lds_rd8(const SeqLds &L, uint32_t p)
+{
+    return (L.data[p >> 2] >> ((p & 3u) * 8u)) & 255u;
+}
+
+__global__ __launch_bounds__(kSeqWaves * 64) void k_lz4_seq(const Batch B)
+{
+    __shared__ SeqLds s_l[kSeqWaves];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t g = blockIdx.x * kSeqWaves + wv;
+    if (g >= B.nsegs) return;
+    SeqLds &L = s_l[wv];
+    const Seg S = B.segs[g];
+    const uint8_t *src = B.base + S.src;
+    const uint32_t n = S.len;
+    for (uint32_t i = lane; i < kSegLZ / 4 + 4; i += 64) {
+        const uint32_t p = 4 * i;
+        uint32_t v = 0;
+        if (p + 4 <= n) {
+            v = ld32u(src + p);
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b)
+                if (p + b < n) v |= uint32_t(src[p + b]) << (8 * b);
+        }
+        L.data[i] = v;
+    }
+    for (uint32_t i = lane; i < (1u << kHashBits); i += 64) L.tab[i] = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    // LZ4 block rules: a match starts >= 12 bytes before the block's end and
+    // the block's last 5 bytes are literals (segments near the end of a block
+    // are limited by the block's end, not their own); and a match's first 4
+    // bytes lie inside the segment.
+    const uint32_t start_lim = min(n >= 4 ? n - 3 : 0u, S.rem > 12 ? S.rem - 12 : 0u);
+    const uint32_t end_lim = min(n, S.rem > 5 ? S.rem - 5 : 0u);
+    uint2 *rec = B.recs + uint64_t(g) * kRecCap;
+    uint32_t cursor = 0, anchor = 0, nrec = 0;
+    while (cursor < start_lim) {
+        const uint32_t p = cursor + lane;
+        const bool valid = p < start_lim;
+        const uint32_t v = valid ? lds_rd32(L, p) : 0u;
+        const uint32_t h = (v * 2654435761u) >> (32 - kHashBits);
+        const uint32_t cand = valid ? L.tab[h] : 0u;
+        const uint32_t c = cand ? cand - 1 : 0u;
+        const bool ok = valid && cand != 0u && c < p && lds_rd32(L, c) == v;
+        const uint64_t m = __ballot(ok);
+        __builtin_amdgcn_wave_barrier();
+        if (!m) {
+            if (valid) L.tab[h] = uint16_t(p + 1);
+            cursor += 64;
+            continue;
+        }
+        const uint32_t f = uint32_t(__ffsll((unsigned long long)m) - 1);
+        const uint32_t q = cursor + f;
+        const uint32_t cq = uint32_t(__builtin_amdgcn_readlane(int(c), int(f)));
+        uint32_t len = 4;
+        for (;;) {
+            const uint32_t i = q + len + lane;
+            const bool eq = i < end_lim && lds_rd8(L, i) == lds_rd8(L, cq + len + lane);
+            const uint64_t mm = __ballot(!eq);
+            if (!mm) {
+                len += 64;
+                continue;
+            }
+            len += uint32_t(__ffsll((unsigned long long)mm) - 1);
+            break;
+        }
+        if (lane == 0) rec[nrec] = make_uint2(q | ((q - cq) << 16), len);
+        ++nrec;
+        // the window's positions before the next cursor enter the table (later
+        // ones are looked up again from there and would only shadow older
+        // candidates)
+        if (valid && p < q + len) L.tab[h] = uint16_t(p + 1);
+        anchor = cursor = q + len;
+    }
+    if (lane == 0) {
+        B.nrec[g] = nrec;
+        B.trail[g] = n - anchor;
+    }
+}
+
+__device__ __forceinline__ uint32_t ext_len(uint32_t x) { return x >= 15 ? (x - 15) / 255 + 1 : 0; }
+
+// ---------------------------------------------------------------------------
+// k_lz4_size / k_lz4_emit: one workgroup per LZ4 block.  A sequence's literal
+// run starts at the previous match's end (or the block start), across segment
+// boundaries; the block ends with a literal-only sequence.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBlkThreads = 256;
+constexpr uint32_t kMaxSegsPerBlk = uint32_t(kBlockLZ / kSegLZ);
+
+struct BlkLds {
+    uint32_t rbase[kMaxSegsPerBlk + 1];  // first record index (block-relative) of each segment
+    uint32_t prev_end[kMaxSegsPerBlk];   // block-relative end of the last match before each segment
+    uint32_t tile_off[kBlkThreads];
+    uint64_t total;
+};
+
+// Block-relative literal start and size of record r of segment s.
+__device__ __forceinline__ void rec_geom(const Batch &B, const Blk &K, const BlkLds &L, uint32_t s, uint32_t r,
+                                         uint32_t &lit_start, uint32_t &lit_len, uint32_t &mpos, uint32_t &off,
+                                         uint32_t &mlen)
+{
+    const uint2 *rec = B.recs + uint64_t(K.seg0 + s) * kRecCap;
+    const uint2 x = rec[r];
+    mpos = s * kSegLZ + (x.x & 0xFFFFu);
+    off = x.x >> 16;
+    mlen = x.y;
+    if (r == 0) {
+        lit_start = L.prev_end[s];
+    } else {
+        const uint2 y = rec[r - 1];
+        lit_start = s * kSegLZ + (y.x & 0xFFFFu) + y.y;
+    }
+    lit_len = mpos - lit_start;
+}
+
+__device__ __forceinline__ uint32_t seq_size(uint32_t lit_len, uint32_t mlen)
+{
+    return 1 + ext_len(lit_len) + lit_len + 2 + ext_len(mlen - 4);
+}
+
+// Shared prologue: per-segment record bases and the match end before each segment.
+__device__ void blk_prologue(const Batch &B, const Blk &K, BlkLds &L)
+{
+    if (threadIdx.x == 0) {
+        uint32_t base = 0, end = 0;
+        for (uint32_t s = 0; s < K.nseg; ++s) {
+            L.rbase[s] = base;
+            L.prev_end[s] = end;
+            const uint32_t nr = B.nrec[K.seg0 + s];
+            if (nr) {
+                const uint2 y = B.recs[uint64_t(K.seg0 + s) * kRecCap + nr - 1];
+                end = s * kSegLZ + (y.x & 0xFFFFu) + y.y;
+            }
+            base += nr;
+        }
+        L.rbase[K.nseg] = base;
+        L.total = end;  // the last match's end: the final literal run starts here
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t seg_of(const BlkLds &L, uint32_t nseg, uint32_t r)
+{
+    uint32_t lo = 0, hi = nseg;  // last s with rbase[s] <= r
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.rbase[mid] <= r) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlkThreads) void k_lz4_size(const Batch B)
+{
+    __shared__ BlkLds L;
+    __shared__ uint64_t s_sum[kBlkThreads / 64];
+    const Blk K = B.blks[blockIdx.x];
+    blk_prologue(B, K, L);
+    const uint32_t nr = L.rbase[K.nseg];
+    const uint32_t last_end = uint32_t(L.total);
+    uint64_t sum = 0;
+    for (uint32_t r = threadIdx.x; r < nr; r += kBlkThreads) {
+        const uint32_t s = seg_of(L, K.nseg, r);
+        uint32_t ls, ll, mp, off, ml;
+        rec_geom(B, K, L, s, r - L.rbase[s], ls, ll, mp, off, ml);
+        sum += seq_size(ll, ml);
+    }
+    for (int o = 32; o; o >>= 1) sum += __shfl_xor(sum, o);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (uint32_t i = 0; i < kBlkThreads / 64; ++i) t += s_sum[i];
+        const uint32_t fl = K.len - last_end;
+        t += 1 + ext_len(fl) + fl;
+        B.blk_size[blockIdx.x] = t < K.len ? uint32_t(t) : (K.len | 0x80000000u);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_enc_plan: one workgroup, serial over blobs in thread 0's hands for the
+// prefix sums (a batch holds at most a few thousand blobs).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_enc_plan(const Batch B)
+{
+    if (threadIdx.x != 0) return;
+    uint64_t out = 0;
+    uint32_t pieces = 0;
+    for (uint32_t b = 0; b < B.nblobs; ++b) {
+        const BlobDesc D = B.blobs[b];
+        uint64_t F;
+        if (B.compress) {
+            uint64_t off = 7;
+            for (uint32_t k = 0; k < D.nblk; ++k) {
+                B.blk_foff[D.blk0 + k] = off;
+                off += 4 + (B.blk_size[D.blk0 + k] & 0x7FFFFFFFu);
+            }
+            F = off + 4 + 4;  // end mark, content checksum
+        } else {
+            F = D.len;
+        }
+        B.frame_len[b] = F;
+        const uint32_t P = B.encrypt ? uint32_t((F + kPiece - 1) / kPiece) : 0u;
+        B.out_off[b] = out;
+        B.piece_base[b] = pieces;
+        out += B.encrypt ? 12 + 48 + F + 28ull * P : F;
+        pieces += P;
+    }
+    B.out_off[B.nblobs] = out;
+    B.piece_base[B.nblobs] = pieces;
+    B.status[0] = out > B.out_cap ? uint64_t(uint32_t(CDC_E_NOSPACE)) : 0ull;
+}
+
+// Where the LZ4 stages write blob b's frame: the frame buffer when it is
+// encrypted next, else its place in the output.
+__device__ __forceinline__ uint8_t *frame_ptr(const Batch &B, uint32_t b)
+{
+    return B.encrypt ? B.frames + B.blobs[b].slot : B.out + B.out_off[b];
+}
+
+// The plaintext the GCM stage seals: the frame, or the blob itself uncompressed.
+__device__ __forceinline__ const uint8_t *plain_ptr(const Batch &B, uint32_t b)
+{
+    return B.compress ? B.frames + B.blobs[b].slot : B.base + B.blobs[b].src;
+}
+
+// Neither compressed nor encrypted: the output is the blob (Encode with no
+// compression and no key configured).
+__global__ __launch_bounds__(256) void k_copy(const Batch B)
+{
+    const uint32_t b = blockIdx.x;
+    if (b >= B.nblobs || B.status[0]) return;
+    const uint8_t *src = B.base + B.blobs[b].src;
+    uint8_t *dst = B.out + B.out_off[b];
+    const uint64_t n = B.blobs[b].len;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
+{
+    __shared__ BlkLds L;
+    if (B.status[0]) return;
+    const Blk K = B.blks[blockIdx.x];
+    uint8_t *dst = frame_ptr(B, K.blob) + B.blk_foff[blockIdx.x];
+    const uint8_t *src = B.base + K.src;
+    const uint32_t bs = B.blk_size[blockIdx.x];
+    if (threadIdx.x == 0) {
+        dst[0] = uint8_t(bs);
+        dst[1] = uint8_t(bs >> 8);
+        dst[2] = uint8_t(bs >> 16);
+        dst[3] = uint8_t(bs >> 24);
+    }
+    dst += 4;
+    if (bs & 0x80000000u) {  // stored: the raw bytes
+        for (uint32_t i = threadIdx.x; i < K.len; i += kBlkThreads) dst[i] = src[i];
+        return;
+    }
+    blk_prologue(B, K, L);
+    const uint32_t nr = L.rbase[K.nseg];
+    const uint32_t last_end = uint32_t(L.total);
+    // tiles of kBlkThreads records: sizes, block-wide exclusive scan, write
+    __shared__ uint32_t s_part[kBlkThreads / 64];
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < nr; t0 += kBlkThreads) {
+        const uint32_t r = t0 + threadIdx.x;
+        uint32_t ls = 0, ll = 0, mp = 0, off = 0, ml = 0, sz = 0;
+        if (r < nr) {
+            const uint32_t s = seg_of(L, K.nseg, r);
+            rec_geom(B, K, L, s, r - L.rbase[s], ls, ll, mp, off, ml);
+            sz = seq_size(ll, ml);
+        }
+        // exclusive scan of sz over the workgroup
+        uint32_t x = sz;
+        const uint32_t lane = threadIdx.x & 63u;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_part[threadIdx.x >> 6] = x;
+        __syncthreads();
+        uint32_t wbase = 0;
+        for (uint32_t i = 0; i < (threadIdx.x >> 6); ++i) wbase += s_part[i];
+        uint32_t tile_total = 0;
+        for (uint32_t i = 0; i < kBlkThreads / 64; ++i) tile_total += s_part[i];
+        __syncthreads();
+        if (r < nr) {
+            uint8_t *o = dst + carry + wbase + x - sz;
+            const uint32_t lt = ll >= 15 ? 15 : ll, mt = ml - 4 >= 15 ? 15 : ml - 4;
+            *o++ = uint8_t(lt << 4 | mt);
+            if (ll >= 15) {
+                uint32_t e = ll - 15;
+                for (; e >= 255; e -= 255) *o++ = 255;
+                *o++ = uint8_t(e);
+            }
+            for (uint32_t i = 0; i < ll; ++i) o[i] = src[ls + i];
+            o += ll;
+            *o++ = uint8_t(off);
+            *o++ = uint8_t(off >> 8);
+            if (ml - 4 >= 15) {
+                uint32_t e = ml - 4 - 15;
+                for (; e >= 255; e -= 255) *o++ = 255;
+                *o++ = uint8_t(e);
+            }
+        }
+        carry += tile_total;
+    }
+    if (threadIdx.x == 0) {  // the final literal-only sequence
+        uint8_t *o = dst + carry;
+        const uint32_t ll = K.len - last_end;
+        *o++ = uint8_t((ll >= 15 ? 15 : ll) << 4);
+        if (ll >= 15) {
+            uint32_t e = ll - 15;
+            for (; e >= 255; e -= 255) *o++ = 255;
+            *o++ = uint8_t(e);
+        }
+        for (uint32_t i = 0; i < ll; ++i) o[i] = src[last_end + i];
+    }
+}
+
+// Frame header (pierrec/lz4 v4 defaults: version 1, independent blocks,
+// content checksum, 4-MiB blocks), end mark and checksum.
+__device__ uint32_t xxh32_small(const uint8_t *p, uint32_t n)
+{
+    uint32_t h = P5 + n;
+    uint32_t i = 0;
+    for (; i + 4 <= n; i += 4) h = rol32(h + ld32u(p + i) * P3, 17) * P4;
+    for (; i < n; ++i) h = rol32(h + p[i] * P5, 11) * P1;
+    h ^= h >> 15;
+    h *= P2;
+    h ^= h >> 13;
+    h *= P3;
+    h ^= h >> 16;
+    return h;
+}
+
+__global__ __launch_bounds__(64) void k_frame_fin(const Batch B)
+{
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= B.nblobs || B.status[0]) return;
+    uint8_t *f = frame_ptr(B, b);
+    const uint8_t hdr[6] = {0x04, 0x22, 0x4D, 0x18, 0x64, 0x70};
+    for (int i = 0; i < 6; ++i) f[i] = hdr[i];
+    f[6] = uint8_t(xxh32_small(hdr + 4, 2) >> 8);
+    const uint64_t F = B.frame_len[b];
+    uint8_t *e = f + F - 8;
+    e[0] = e[1] = e[2] = e[3] = 0;
+    const uint32_t x = B.xxh[b];
+    e[4] = uint8_t(x);
+    e[5] = uint8_t(x >> 8);
+    e[6] = uint8_t(x >> 16);
+    e[7] = uint8_t(x >> 24);
+}
+
+// ---------------------------------------------------------------------------
+// GCM
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void gcm_block_words(const uint8_t *p, uint32_t w[4])
+{
+    for (int i = 0; i < 4; ++i)
+        w[i] = uint32_t(p[4 * i]) << 24 | uint32_t(p[4 * i + 1]) << 16 | uint32_t(p[4 * i + 2]) << 8 | p[4 * i + 3];
+}
+
+// One lane: Seal(key, nonce, pt[0..32)) -> ct (32) || tag (16), for the
+// subkey header (two blocks, no AAD).
+__device__ void seal32(const uint32_t rk[60], const uint8_t nonce[12], const uint8_t pt[32], uint8_t *out)
+{
+    uint32_t z[4] = {0, 0, 0, 0};
+    aes256_block(rk, g_te0, g_sbox, z);
+    G128 th[16];
+    gtable(g_from_words(z), th);
+    uint32_t j0[4];
+    j0[0] = uint32_t(nonce[0]) << 24 | uint32_t(nonce[1]) << 16 | uint32_t(nonce[2]) << 8 | nonce[3];
+    j0[1] = uint32_t(nonce[4]) << 24 | uint32_t(nonce[5]) << 16 | uint32_t(nonce[6]) << 8 | nonce[7];
+    j0[2] = uint32_t(nonce[8]) << 24 | uint32_t(nonce[9]) << 16 | uint32_t(nonce[10]) << 8 | nonce[11];
+    j0[3] = 1;
+    G128 S = {0, 0};
+    for (uint32_t i = 0; i < 2; ++i) {
+        uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
+        aes256_block(rk, g_te0, g_sbox, c);
+        uint32_t p[4];
+        gcm_block_words(pt + 16 * i, p);
+        for (int k = 0; k < 4; ++k) {
+            c[k] ^= p[k];
+            out[16 * i + 4 * k] = uint8_t(c[k] >> 24);
+            out[16 * i + 4 * k + 1] = uint8_t(c[k] >> 16);
+            out[16 * i + 4 * k + 2] = uint8_t(c[k] >> 8);
+            out[16 * i + 4 * k + 3] = uint8_t(c[k]);
+        }
+        S = gmul4(gx(S, g_from_words(c)), th);
+    }
+    S = gmul4(gx(S, G128{0, 256}), th);  // len(A) = 0, len(C) = 256 bits
+    uint32_t t[4] = {j0[0], j0[1], j0[2], j0[3]};
+    aes256_block(rk, g_te0, g_sbox, t);
+    const uint64_t hi = S.hi ^ (uint64_t(t[0]) << 32 | t[1]), lo = S.lo ^ (uint64_t(t[2]) << 32 | t[3]);
+    for (int k = 0; k < 8; ++k) {
+        out[32 + k] = uint8_t(hi >> (56 - 8 * k));
+        out[40 + k] = uint8_t(lo >> (56 - 8 * k));
+    }
+}
+
+__global__ __launch_bounds__(64) void k_blob_keys(const Batch B)
+{
+    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= B.nblobs || B.status[0]) return;
+    const uint8_t *r = B.rnd + 56ull * b;  // subkey 32, subkey nonce 12, data nonce 12
+    BlobKey &K = B.keys[b];
+    uint32_t rk[60];
+    aes256_expand(r, rk, g_sbox);
+    for (int i = 0; i < 60; ++i) K.rk[i] = rk[i];
+    uint32_t z[4] = {0, 0, 0, 0};
+    aes256_block(rk, g_te0, g_sbox, z);
+    const G128 H = g_from_words(z);
+    G128 th[16];
+    gtable(H, th);
+    for (int i = 0; i < 16; ++i) K.th[i] = th[i];
+    G128 p = H;
+    K.hpow[0] = H;
+    for (int e = 1; e < 64; ++e) {
+        p = gmul4(p, th);
+        K.hpow[e] = p;
+    }
+    G128 t64[16];
+    gtable(p, t64);
+    for (int i = 0; i < 16; ++i) K.th64[i] = t64[i];
+    // header: subkey nonce || Seal(repository key, subkey nonce, subkey)
+    uint8_t *o = B.out + B.out_off[b];
+    for (int i = 0; i < 12; ++i) o[i] = r[32 + i];
+    uint32_t mk[60];
+    uint8_t key[32];
+    for (int i = 0; i < 32; ++i) key[i] = B.key[i];
+    aes256_expand(key, mk, g_sbox);
+    seal32(mk, r + 32, r, o + 12);
+}
+
+constexpr uint32_t kGcmWaves = 4;
+
+struct GcmLds {
+    uint32_t te[256];
+    uint8_t sb[256];
+    struct PerWave {
+        uint32_t rk[60];
+        G128 th64[16];
+        G128 th[16];
+    } w[kGcmWaves];
+};
+
+__global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
+{
+    __shared__ GcmLds L;
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        L.te[i] = g_te0[i];
+        L.sb[i] = g_sbox[i];
+    }
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t pc = blockIdx.x * kGcmWaves + wv;
+    const uint32_t total = B.piece_base[B.nblobs];
+    const bool active = pc < total && !B.status[0];
+    uint32_t b = 0;
+    if (active) {
+        uint32_t lo = 0, hi = B.nblobs;  // last blob with piece_base <= pc
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (B.piece_base[mid] <= pc) lo = mid;
+            else hi = mid;
+        }
+        b = lo;
+        const BlobKey &K = B.keys[b];
+        for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk[i] = K.rk[i];
+        if (lane < 16) {
+            L.w[wv].th64[lane] = K.th64[lane];
+            L.w[wv].th[lane] = K.th[lane];
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const BlobKey &K = B.keys[b];
+    const uint32_t k = pc - B.piece_base[b];
+    const uint64_t F = B.frame_len[b];
+    const uint64_t p0 = uint64_t(k) * kPiece;
+    const uint32_t m = uint32_t(min<uint64_t>(kPiece, F - p0));  // piece bytes
+    const uint32_t nb = (m + 15) / 16;
+    const uint8_t *pt = plain_ptr(B, b) + p0;
+    uint8_t *o = B.out + B.out_off[b] + 60 + uint64_t(k) * (kPiece + 28);
+    const uint8_t *dn = B.rnd + 56ull * b + 44;  // data nonce
+    uint32_t j0[3];
+    j0[0] = uint32_t(dn[0]) << 24 | uint32_t(dn[1]) << 16 | uint32_t(dn[2]) << 8 | dn[3];
+    j0[1] = uint32_t(dn[4]) << 24 | uint32_t(dn[5]) << 16 | uint32_t(dn[6]) << 8 | dn[7];
+    j0[2] = (uint32_t(dn[8]) << 24 | uint32_t(dn[9]) << 16 | uint32_t(dn[10]) << 8 | dn[11]) ^ k;
+    if (lane < 12) o[lane] = uint8_t(j0[lane >> 2] >> (24 - 8 * (lane & 3)));
+    uint8_t *ct = o + 12;
+    const uint32_t *rk = L.w[wv].rk;
+    // lane: blocks lane, lane + 64, ...; Horner in H^64
+    G128 Z = {0, 0};
+    uint32_t cnt = 0;
+    for (uint32_t i = lane; i < nb; i += 64) {
+        uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
+        aes256_block(rk, L.te, L.sb, c);
+        const uint32_t bytes = min(16u, m - 16 * i);
+        uint8_t blk[16];
+        for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
+        uint32_t w[4];
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pw = uint32_t(blk[4 * q]) << 24 | uint32_t(blk[4 * q + 1]) << 16 |
+                                uint32_t(blk[4 * q + 2]) << 8 | blk[4 * q + 3];
+            w[q] = c[q] ^ pw;
+        }
+        uint8_t cb[16];
+        for (int q = 0; q < 4; ++q) {
+            cb[4 * q] = uint8_t(w[q] >> 24);
+            cb[4 * q + 1] = uint8_t(w[q] >> 16);
+            cb[4 * q + 2] = uint8_t(w[q] >> 8);
+            cb[4 * q + 3] = uint8_t(w[q]);
+        }
+        for (uint32_t q = 0; q < bytes; ++q) ct[16 * i + q] = cb[q];
+        if (bytes < 16)
+            for (uint32_t q = bytes; q < 16; ++q) cb[q] = 0;
+        uint32_t cw[4];
+        gcm_block_words(cb, cw);
+        Z = gx(gmul4(Z, L.w[wv].th64), g_from_words(cw));
+        ++cnt;
+    }
+    if (cnt) {
+        const uint32_t e = nb - lane - 64 * (cnt - 1);  // 1..64
+        Z = gmul_bits(Z, K.hpow[e - 1]);
+    }
+    for (int off = 32; off; off >>= 1) {
+        Z.hi ^= __shfl_xor(Z.hi, off);
+        Z.lo ^= __shfl_xor(Z.lo, off);
+    }
+    if (lane == 0) {
+        G128 S = gmul4(gx(Z, G128{0, uint64_t(m) * 8}), L.w[wv].th);
+        uint32_t t[4] = {j0[0], j0[1], j0[2], 1};
+        aes256_block(rk, L.te, L.sb, t);
+        const uint64_t hi = S.hi ^ (uint64_t(t[0]) << 32 | t[1]), lo = S.lo ^ (uint64_t(t[2]) << 32 | t[3]);
+        uint8_t *tag = ct + m;
+        for (int q = 0; q < 8; ++q) {
+            tag[q] = uint8_t(hi >> (56 - 8 * q));
+            tag[8 + q] = uint8_t(lo >> (56 - 8 * q));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+static std::once_flag g_tab_once;
+static int g_tab_status = CDC_OK;
+
+static int ensure_tables()
+{
+    std::call_once(g_tab_once, [] {
+        uint32_t te0[256];
+        uint8_t sbox[256];
+        build_tables(te0, sbox);
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) {
+            g_tab_status = CDC_E_DEVICE;
+            return;
+        }
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        for (int d = 0; d < n; ++d) {
+            if (hipSetDevice(d) != hipSuccess || hipMemcpyToSymbol(HIP_SYMBOL(g_te0), te0, sizeof(te0)) != hipSuccess ||
+                hipMemcpyToSymbol(HIP_SYMBOL(g_sbox), sbox, sizeof(sbox)) != hipSuccess)
+                g_tab_status = CDC_E_DEVICE;
+        }
+        (void)hipSetDevice(cur);
+    });
+    return g_tab_status;
+}
+
+static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+
+}  // namespace enc
+
+using namespace enc;
+
+// Device-resident encode of n blobs (see include/plakar_cdc.h).
+extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t *offsets, const uint64_t *lens,
+                                 uint32_t n, int compress, const uint8_t *key, const uint8_t *random, uint8_t *d_out,
+                                 uint64_t out_cap, uint64_t *out_offsets, void *stream)
+{
+    if ((n && (!d_base || !offsets || !lens || !out_offsets)) || (key && !random) || !d_out) return CDC_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    int st = ensure_tables();
+    if (st != CDC_OK) return st;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool encrypt = key != nullptr;
+    // plan on the host: blobs, 4-MiB blocks, 16-KiB segments, frame slots
+    std::vector<BlobDesc> blobs(n);
+    std::vector<Blk> blks;
+    std::vector<Seg> segs;
+    uint64_t slot = 0, pieces_max = 0;
+    for (uint32_t b = 0; b < n; ++b) {
+        BlobDesc &D = blobs[b];
+        D.src = offsets[b];
+        D.len = lens[b];
+        D.blk0 = uint32_t(blks.size());
+        D.nblk = compress ? uint32_t((lens[b] + kBlockLZ - 1) / kBlockLZ) : 0u;
+        for (uint32_t k = 0; k < D.nblk; ++k) {
+            Blk K{};
+            K.src = offsets[b] + k * kBlockLZ;
+            K.len = uint32_t(std::min<uint64_t>(kBlockLZ, lens[b] - k * kBlockLZ));
+            K.blob = b;
+            K.k = k;
+            K.seg0 = uint32_t(segs.size());
+            K.nseg = (K.len + kSegLZ - 1) / kSegLZ;
+            for (uint32_t g = 0; g < K.nseg; ++g) {
+                Seg S{};
+                S.src = K.src + uint64_t(g) * kSegLZ;
+                S.len = std::min<uint32_t>(kSegLZ, K.len - g * kSegLZ);
+                S.rem = K.len - g * kSegLZ;
+                segs.push_back(S);
+            }
+            blks.push_back(K);
+        }
+        const uint64_t fmax = compress ? 7 + 4ull * D.nblk + lens[b] + 8 : lens[b];
+        D.slot = slot;
+        slot += align16(fmax);
+        pieces_max += encrypt ? (fmax + kPiece - 1) / kPiece : 0;
+    }
+    // one device allocation for the plan and the workspace
+    const size_t nb = blobs.size(), nk = blks.size(), ng = segs.size();
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = align16(off + bytes);
+        return o;
+    };
+    const size_t o_blobs = take(nb * sizeof(BlobDesc)), o_blks = take(nk * sizeof(Blk)), o_segs = take(ng * sizeof(Seg));
+    const size_t o_rnd = take(encrypt ? nb * 56 : 0), o_key = take(32);
+    const size_t o_recs = take(ng * kRecCap * sizeof(uint2)), o_nrec = take(ng * 4), o_trail = take(ng * 4);
+    const size_t o_bsz = take(nk * 4), o_bfo = take(nk * 8), o_xxh = take(nb * 4), o_flen = take(nb * 8);
+    const size_t o_oo = take((nb + 1) * 8), o_pb = take((nb + 1) * 4), o_keys = take(encrypt ? nb * sizeof(BlobKey) : 0);
+    const size_t o_status = take(8), o_frames = take(encrypt ? slot : 0);
+    uint8_t *ws = nullptr;
+    if (hipMalloc(&ws, off ? off : 16) != hipSuccess) return CDC_E_DEVICE;
+    Batch Bt{};
+    Bt.base = static_cast<const uint8_t *>(d_base);
+    Bt.nblobs = n;
+    Bt.nsegs = uint32_t(ng);
+    Bt.nblks = uint32_t(nk);
+    Bt.npieces_max = uint32_t(pieces_max);
+    Bt.compress = compress ? 1u : 0u;
+    Bt.encrypt = encrypt ? 1u : 0u;
+    Bt.blobs = reinterpret_cast<BlobDesc *>(ws + o_blobs);
+    Bt.blks = reinterpret_cast<Blk *>(ws + o_blks);
+    Bt.segs = reinterpret_cast<Seg *>(ws + o_segs);
+    Bt.rnd = ws + o_rnd;
+    Bt.key = ws + o_key;
+    Bt.frames = ws + o_frames;
+    Bt.out = d_out;
+    Bt.out_cap = out_cap;
+    Bt.recs = reinterpret_cast<uint2 *>(ws + o_recs);
+    Bt.nrec = reinterpret_cast<uint32_t *>(ws + o_nrec);
+    Bt.trail = reinterpret_cast<uint32_t *>(ws + o_trail);
+    Bt.blk_size = reinterpret_cast<uint32_t *>(ws + o_bsz);
+    Bt.blk_foff = reinterpret_cast<uint64_t *>(ws + o_bfo);
+    Bt.xxh = reinterpret_cast<uint32_t *>(ws + o_xxh);
+    Bt.frame_len = reinterpret_cast<uint64_t *>(ws + o_flen);
+    Bt.out_off = reinterpret_cast<uint64_t *>(ws + o_oo);
+    Bt.piece_base = reinterpret_cast<uint32_t *>(ws + o_pb);
+    Bt.keys = reinterpret_cast<BlobKey *>(ws + o_keys);
+    Bt.status = reinterpret_cast<uint64_t *>(ws + o_status);
+    bool ok = true;
+    auto h2d = [&](size_t o, const void *p, size_t bytes) {
+        if (bytes) ok = ok && hipMemcpyAsync(ws + o, p, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+    };
+    h2d(o_blobs, blobs.data(), nb * sizeof(BlobDesc));
+    h2d(o_blks, blks.data(), nk * sizeof(Blk));
+    h2d(o_segs, segs.data(), ng * sizeof(Seg));
+    if (encrypt) {
+        h2d(o_rnd, random, nb * 56);
+        h2d(o_key, key, 32);
+    }
+    if (ok && n) {
+        if (compress) {
+            hipLaunchKernelGGL(k_xxh32, dim3((n + 3) / 4), dim3(256), 0, s, Bt);
+            if (ng) hipLaunchKernelGGL(k_lz4_seq, dim3(uint32_t((ng + kSeqWaves - 1) / kSeqWaves)), dim3(kSeqWaves * 64), 0, s, Bt);
+            if (nk) hipLaunchKernelGGL(k_lz4_size, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
+        }
+        hipLaunchKernelGGL(k_enc_plan, dim3(1), dim3(64), 0, s, Bt);
+        if (encrypt) hipLaunchKernelGGL(k_blob_keys, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
+        if (compress) {
+            if (nk) hipLaunchKernelGGL(k_lz4_emit, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
+            hipLaunchKernelGGL(k_frame_fin, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
+        } else if (!encrypt) {
+            hipLaunchKernelGGL(k_copy, dim3(n), dim3(256), 0, s, Bt);
+        }
+        if (encrypt && pieces_max)
+            hipLaunchKernelGGL(k_gcm, dim3(uint32_t((pieces_max + kGcmWaves - 1) / kGcmWaves)), dim3(kGcmWaves * 64), 0, s, Bt);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    uint64_t status = 0;
+    if (ok) {
+        if (n) {
+            ok = hipMemcpyAsync(out_offsets, ws + o_oo, (nb + 1) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                 hipMemcpyAsync(&status, ws + o_status, 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+        } else {
+            out_offsets[0] = 0;
+        }
+        ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    }
+    (void)hipFree(ws);
+    if (!ok) return CDC_E_DEVICE;
+    return status ? int(int32_t(uint32_t(status))) : CDC_OK;
+}
+
+extern "C" uint64_t cdc_encode_bound(uint64_t len, int compress, int encrypt)
+{
+    const uint64_t f = compress ? 7 + 4 * ((len + kBlockLZ - 1) / kBlockLZ) + len + 8 : len;
+    return encrypt ? 60 + f + 28 * ((f + kPiece - 1) / kPiece) : f;
+}

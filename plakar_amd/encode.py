@@ -1,0 +1,62 @@
+"""Encode on the device: plakar's (*Repository).Encode (repository/repository.go:
+212-236) for a batch of blobs -- the LZ4 frame of compression.DeflateLZ4Stream
+(compression/compression.go:94-106), then the AES-256-GCM stream of
+encryption.EncryptStream (encryption/symmetric.go:72-163) when a key is
+configured.  Every call goes through the C ABI (cdc_encode_device)."""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ensure_init, lib
+
+RANDOM_BYTES = 56  # per blob: subkey 32, subkey nonce 12, data nonce 12
+
+
+def encode_bound(n, compress=True, encrypt=True):
+    return int(lib().cdc_encode_bound(int(n), int(bool(compress)), int(bool(encrypt))))
+
+
+def encode_device(base, offsets, lens, out, key=None, compress=True, random=None, device=0, stream=None):
+    """Encode blobs that live in the device tensor `base` (uint8) at the given
+    byte offsets/lengths into the device tensor `out`; returns the n + 1
+    output offsets."""
+    import torch
+    ensure_init()
+    n = len(lens)
+    offs = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in offsets])
+    lns = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
+    oo = (ctypes.c_uint64 * (n + 1))()
+    if key is not None:
+        key = bytes(key)
+        if len(key) != 32:
+            raise ValueError("the repository key is 32 bytes (AES-256)")
+        if random is None:
+            random = os.urandom(RANDOM_BYTES * n)
+        if len(random) != RANDOM_BYTES * n:
+            raise ValueError(f"random: {RANDOM_BYTES} bytes per blob")
+    st = stream if stream is not None else torch.cuda.current_stream(device)
+    check(lib().cdc_encode_device(int(device), ctypes.c_void_p(base.data_ptr()), offs, lns, n, int(bool(compress)),
+                                  key, bytes(random) if key is not None else None, ctypes.c_void_p(out.data_ptr()),
+                                  out.numel(), oo, ctypes.c_void_p(st.cuda_stream)), "cdc_encode_device")
+    return [int(oo[i]) for i in range(n + 1)]
+
+
+def encode_blobs(blobs, key=None, compress=True, random=None, device=0):
+    """Encode host byte buffers (numpy uint8 arrays or bytes): a list of the
+    encoded bytes, blob by blob."""
+    import torch
+    arrs = [np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray)) else np.asarray(b, np.uint8).ravel()
+            for b in blobs]
+    lens = [a.size for a in arrs]
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) if arrs else np.zeros(1, np.uint64)
+    dev = torch.device("cuda", device)
+    base = torch.empty(max(int(offs[-1]), 1), dtype=torch.uint8, device=dev)
+    if arrs and offs[-1]:
+        base[:int(offs[-1])].copy_(torch.from_numpy(np.concatenate(arrs)))
+    cap = sum(encode_bound(n, compress, key is not None) for n in lens)
+    out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+    oo = encode_device(base, offs[:-1], lens, out, key=key, compress=compress, random=random, device=device)
+    host = out[:oo[-1]].cpu().numpy()
+    return [host[oo[i]:oo[i + 1]].tobytes() for i in range(len(lens))]

@@ -1,0 +1,152 @@
+"""Device Encode: plakar's (*Repository).Encode --
+the LZ4 frame of compression.DeflateLZ4Stream, then the AES-256-GCM stream of
+encryption.EncryptStream -- checked with independent decoders (the system's
+liblz4 and OpenSSL libcrypto, tests/crypto_ref.py) and the NIST SP 800-38D
+AES-256 test vectors.  Nonces and subkeys are random in the reference, so the
+encrypted bytes are checked by round trip and by structure; the AES-GCM
+arithmetic itself is pinned by the vectors."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import crypto_ref as ref  # noqa: E402
+from datagen import low_entropy, random_bytes  # noqa: E402
+from plakar_amd import _lib, encode  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+KEY = bytes(range(32))
+
+# NIST GCM test vectors, AES-256 (test cases 13-15 of the GCM specification).
+NIST = [
+    (bytes(32), bytes(12), b"", "", "530f8afbc74536b9a963b4f1c4cb738b"),
+    (bytes(32), bytes(12), bytes(16), "cea7403d4d606b6e074ec5d3baf39d18", "d0d1c8a799996bf0265b98b5d48ab919"),
+    (bytes.fromhex("feffe9928665731c6d6a8f9467308308feffe9928665731c6d6a8f9467308308"),
+     bytes.fromhex("cafebabefacedbaddecaf888"),
+     bytes.fromhex("d9313225f88406e5a55909c5aff5269a86a7a9531534f7da2e4c303d8a318a72"
+                   "1c3c0c95956809532fcf0e2449a6b525b16aedf5aa0de657ba637b391aafd255"),
+     "522dc1f099567d07f47f37a32a84427d643a8cdcbfe5c0c97598a2bd2555d1aa"
+     "8cb08e48590dbb3da7b08b1056828838c5f61e6393ba7a0abcc9f662898015ad",
+     "b094dac5d93471bdec1a502270e3cc6c"),
+]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _init():
+    _lib.ensure_init()
+
+
+@pytest.mark.parametrize("case", range(len(NIST)))
+def test_gcm_nist_vectors(case):
+    """Encode without compression, the blob sealed under subkey = the vector's
+    key with data nonce = its IV: the first piece is exactly IV || C || T; the
+    header opens under the repository key to that subkey."""
+    k, iv, p, c, t = NIST[case]
+    rnd = k + bytes(range(100, 112)) + iv  # subkey, subkey nonce, data nonce
+    (out,) = encode.encode_blobs([p], key=KEY, compress=False, random=rnd)
+    assert out[:12] == bytes(range(100, 112))
+    assert ref.gcm_open(KEY, out[:12], out[12:60]) == k
+    if p:
+        assert out[60:72] == iv
+        assert out[72:].hex() == c + t
+    else:
+        assert len(out) == 60  # EncryptStream writes no piece for an empty stream
+        assert ref.gcm_seal(k, iv, b"").hex() == t  # the checker itself, on the empty vector
+
+
+def test_gcm_against_libcrypto_pieces():
+    """Multi-piece streams (64-KiB pieces, a short last one) against
+    libcrypto, piece by piece, with the per-piece nonce rule."""
+    blob = random_bytes(3 * 65536 + 1000, 31).tobytes()
+    rnd = os.urandom(56)
+    (out,) = encode.encode_blobs([blob], key=KEY, compress=False, random=rnd)
+    sub, dn = rnd[:32], rnd[44:56]
+    pos, k = 60, 0
+    while pos < len(out):
+        nonce = dn[:8] + (int.from_bytes(dn[8:], "big") ^ k).to_bytes(4, "big")
+        piece = blob[k * 65536:(k + 1) * 65536]
+        assert out[pos:pos + 12] == nonce
+        assert out[pos + 12:pos + 12 + len(piece) + 16] == ref.gcm_seal(sub, nonce, piece)
+        pos += 12 + len(piece) + 16
+        k += 1
+    assert k == 4 and pos == len(out)
+
+
+SIZES = [0, 1, 15, 16, 17, 4095, 16384, 16385, 65535, 65536, 65537, (1 << 20) + 13, 4 << 20, (4 << 20) + 1,
+         (9 << 20) + 77]
+
+
+def _blobs(kind):
+    out = []
+    for i, n in enumerate(SIZES):
+        if kind == "random":
+            out.append(random_bytes(n, 500 + i).tobytes())
+        elif kind == "low":
+            out.append(low_entropy(n, 600 + i).tobytes())
+        else:  # text-like: repeated words with variation
+            words = [b"backup ", b"snapshot ", b"chunk ", b"packfile ", b"plakar ", b"%d " % i]
+            r = np.random.default_rng(i)
+            s = b"".join(words[j] for j in r.integers(0, len(words), size=n // 4 + 1))
+            out.append(s[:n])
+    return out
+
+
+@pytest.mark.parametrize("kind", ["random", "low", "text"])
+def test_lz4_frames_decode_with_liblz4(kind):
+    """Compression only: every frame decodes with liblz4 (block sizes,
+    content checksum) to the blob; the header is pierrec/lz4 v4's default
+    (FLG 0x64: version 1, independent blocks, content checksum; BD 0x70:
+    4-MiB blocks); compressible data shrinks."""
+    import xxhash
+    blobs = _blobs(kind)
+    outs = encode.encode_blobs(blobs, key=None, compress=True)
+    for b, o in zip(blobs, outs):
+        assert o[:4] == struct.pack("<I", 0x184D2204) and o[4] == 0x64 and o[5] == 0x70
+        assert o[6] == (xxhash.xxh32(o[4:6]).intdigest() >> 8) & 0xFF
+        assert o[-4:] == struct.pack("<I", xxhash.xxh32(b).intdigest())
+        assert ref.lz4f_decompress(o) == b, f"{len(b)} bytes"
+    total_in = sum(len(b) for b in blobs)
+    total_out = sum(len(o) for o in outs)
+    if kind == "random":
+        assert total_out <= total_in + 19 * len(blobs) + 4 * 5  # stored blocks
+    else:
+        assert total_out < 0.5 * total_in, (total_out, total_in)
+
+
+@pytest.mark.parametrize("compress", [True, False])
+def test_encode_roundtrip(compress):
+    """The whole Encode: DecryptStream (restated over libcrypto) then the LZ4
+    frame reader (liblz4) give back every blob; random material from the
+    OS CSPRNG, as the reference's crypto/rand."""
+    blobs = _blobs("text")[:10] + _blobs("random")[8:12]
+    outs = encode.encode_blobs(blobs, key=KEY, compress=compress)
+    for b, o in zip(blobs, outs):
+        assert ref.decode(o, key=KEY, compressed=compress) == b
+        with pytest.raises(ValueError):  # a flipped ciphertext bit fails its tag
+            bad = bytearray(o)
+            bad[-1] ^= 1
+            ref.decode(bytes(bad), key=KEY, compressed=compress)
+
+
+def test_encode_device_resident_batch():
+    """The device entry point over blobs at arbitrary offsets of one buffer
+    (a chunked file's cut list), output offsets as documented."""
+    data = low_entropy(12 << 20, 77)
+    t = torch.from_numpy(data).cuda()
+    cuts = [(0, 70_000), (70_000, 1 << 20), ((1 << 20) + 70_000, 3 << 20), ((4 << 20) + 70_000, 5_000_000),
+            (12 << 20, 0)]
+    offs, lens = [c[0] for c in cuts], [c[1] for c in cuts]
+    cap = sum(encode.encode_bound(n) for n in lens)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    oo = encode.encode_device(t, offs, lens, out, key=KEY)
+    host = out.cpu().numpy()
+    for i, (o, n) in enumerate(cuts):
+        enc = host[oo[i]:oo[i + 1]].tobytes()
+        assert ref.decode(enc, key=KEY) == data[o:o + n].tobytes()
+    small = torch.empty(oo[-1] - 1, dtype=torch.uint8, device="cuda")
+    with pytest.raises(_lib.CdcError):
+        encode.encode_device(t, offs, lens, small, key=KEY)
