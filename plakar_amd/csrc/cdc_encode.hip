@@ -17,7 +17,7 @@
 //   k_lz4_size    one workgroup per 4-MiB LZ4 block: literal runs across
 //                 segment boundaries, encoded size (raw when not smaller)
 //   k_enc_plan    one workgroup: frame sizes, block offsets in the frame,
-//                 GCM pieces and output offsets of every blob
+//                 GCM pieces and output offsets of every blob (scans)
 //   k_lz4_emit    one workgroup per block: the block's bytes in the frame
 //   k_frame_fin   one wave per blob: frame header, end mark, checksum
 //   k_blob_keys   one lane per blob: the subkey's round keys, H and its
@@ -288,25 +288,66 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t *p)  // unaligned
 // ---------------------------------------------------------------------------
 constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u, P5 = 374761393u;
 
-__global__ __launch_bounds__(256) void k_xxh32(const Batch B)
+// The stripes stream through LDS 4 KiB at a time (double-buffered: the whole
+// wave loads region r + 1 while lanes 0-3 run their chains over region r), so
+// the accumulators' dependent multiply chain, not memory latency, sets the pace.
+constexpr uint32_t kXxWaves = 4;
+constexpr uint32_t kXxRegion = 4096;
+
+__global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
 {
-    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    __shared__ uint32_t s_buf[kXxWaves][2][kXxRegion / 4];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kXxWaves + wv;
     if (w >= B.nblobs) return;
     const BlobDesc D = B.blobs[w];
     const uint8_t *p = B.base + D.src;
-    const uint64_t n = D.len, stripes = n / 16;
-    uint32_t v = 0;
-    if (lane < 4) {
-        v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0u : 0u - P1;
-        uint64_t s = 0;
-        for (; s + 8 <= stripes; s += 8) {
-            uint32_t in[8];
+    const uint64_t n = D.len, stripes = n / 16, nwords = stripes * 4;
+    const uint32_t *A = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u) * 8u;
+    const uint64_t R = (stripes * 16 + kXxRegion - 1) / kXxRegion;
+    uint32_t pw[16];
+    auto prefetch = [&](uint64_t r) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) in[j] = ld32u(p + 16 * (s + j) + 4 * lane);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v = rol32(v + in[j] * P2, 13) * P1;
+        for (uint32_t i = 0; i < 16; ++i) {
+            const uint64_t k = r * (kXxRegion / 4) + 16 * lane + i;  // blob word
+            uint32_t x = 0;
+            if (k < nwords) {
+                x = A[k];
+                // misaligned: the next aligned word holds the word's last bytes (never past them)
+                if (sh) x = __builtin_amdgcn_alignbit(A[k + 1], x, sh);
+            }
+            pw[i] = x;
         }
-        for (; s < stripes; ++s) v = rol32(v + ld32u(p + 16 * s + 4 * lane) * P2, 13) * P1;
+    };
+    auto store = [&](uint64_t r) {
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) s_buf[wv][r & 1][16 * lane + i] = pw[i];
+    };
+    uint32_t v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0u : 0u - P1;
+    if (R) {
+        prefetch(0);
+        store(0);
+    }
+    for (uint64_t r = 0; r < R; ++r) {
+        if (r + 1 < R) prefetch(r + 1);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): region r is in LDS
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 4) {
+            const uint32_t *bw = s_buf[wv][r & 1];
+            const uint32_t ns = uint32_t(min<uint64_t>(kXxRegion / 16, stripes - r * (kXxRegion / 16)));
+            uint32_t s = 0;
+            for (; s + 8 <= ns; s += 8) {
+                uint32_t in[8];
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) in[j] = bw[4 * (s + j) + lane];
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) v = rol32(v + in[j] * P2, 13) * P1;
+            }
+            for (; s < ns; ++s) v = rol32(v + bw[4 * s + lane] * P2, 13) * P1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (r + 1 < R) store(r + 1);
     }
     const uint32_t v1 = __shfl(v, 0), v2 = __shfl(v, 1), v3 = __shfl(v, 2), v4 = __shfl(v, 3);
     if (lane != 0) return;
@@ -524,37 +565,88 @@ __global__ __launch_bounds__(kBlkThreads) void k_lz4_size(const Batch B)
 }
 
 // ---------------------------------------------------------------------------
-// k_enc_plan: one workgroup, serial over blobs in thread 0's hands for the
-// prefix sums (a batch holds at most a few thousand blobs).
+// k_enc_plan: one workgroup of 1,024 threads: per blob its frame size (and the
+// offsets of its blocks in the frame), GCM pieces and output size; then
+// exclusive scans over the blobs, tile by tile.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_enc_plan(const Batch B)
+constexpr uint32_t kPlanThreads = 1024;
+
+__global__ __launch_bounds__(kPlanThreads) void k_enc_plan(const Batch B)
 {
-    if (threadIdx.x != 0) return;
-    uint64_t out = 0;
-    uint32_t pieces = 0;
-    for (uint32_t b = 0; b < B.nblobs; ++b) {
-        const BlobDesc D = B.blobs[b];
-        uint64_t F;
-        if (B.compress) {
-            uint64_t off = 7;
-            for (uint32_t k = 0; k < D.nblk; ++k) {
-                B.blk_foff[D.blk0 + k] = off;
-                off += 4 + (B.blk_size[D.blk0 + k] & 0x7FFFFFFFu);
-            }
-            F = off + 4 + 4;  // end mark, content checksum
-        } else {
-            F = D.len;
-        }
-        B.frame_len[b] = F;
-        const uint32_t P = B.encrypt ? uint32_t((F + kPiece - 1) / kPiece) : 0u;
-        B.out_off[b] = out;
-        B.piece_base[b] = pieces;
-        out += B.encrypt ? 12 + 48 + F + 28ull * P : F;
-        pieces += P;
+    __shared__ uint64_t s_o[kPlanThreads / 64];
+    __shared__ uint32_t s_p[kPlanThreads / 64];
+    __shared__ uint64_t s_carry_o;
+    __shared__ uint32_t s_carry_p;
+    if (threadIdx.x == 0) {
+        s_carry_o = 0;
+        s_carry_p = 0;
     }
-    B.out_off[B.nblobs] = out;
-    B.piece_base[B.nblobs] = pieces;
-    B.status[0] = out > B.out_cap ? uint64_t(uint32_t(CDC_E_NOSPACE)) : 0ull;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint32_t t0 = 0; t0 < B.nblobs; t0 += kPlanThreads) {
+        const uint32_t b = t0 + threadIdx.x;
+        uint64_t O = 0;
+        uint32_t P = 0;
+        if (b < B.nblobs) {
+            const BlobDesc D = B.blobs[b];
+            uint64_t F;
+            if (B.compress) {
+                uint64_t off = 7;
+                for (uint32_t k = 0; k < D.nblk; ++k) {
+                    B.blk_foff[D.blk0 + k] = off;
+                    off += 4 + (B.blk_size[D.blk0 + k] & 0x7FFFFFFFu);
+                }
+                F = off + 4 + 4;  // end mark, content checksum
+            } else {
+                F = D.len;
+            }
+            B.frame_len[b] = F;
+            P = B.encrypt ? uint32_t((F + kPiece - 1) / kPiece) : 0u;
+            O = B.encrypt ? 12 + 48 + F + 28ull * P : F;
+        }
+        uint64_t xo = O;
+        uint32_t xp = P;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t yo = __shfl_up(xo, d);
+            const uint32_t yp = __shfl_up(xp, d);
+            if (lane >= d) {
+                xo += yo;
+                xp += yp;
+            }
+        }
+        if (lane == 63) {
+            s_o[wv] = xo;
+            s_p[wv] = xp;
+        }
+        __syncthreads();
+        uint64_t bo = s_carry_o;
+        uint32_t bp = s_carry_p;
+        for (uint32_t i = 0; i < wv; ++i) {
+            bo += s_o[i];
+            bp += s_p[i];
+        }
+        if (b < B.nblobs) {
+            B.out_off[b] = bo + xo - O;
+            B.piece_base[b] = bp + xp - P;
+        }
+        __syncthreads();
+        if (threadIdx.x == kPlanThreads - 1) {
+            uint64_t to = 0;
+            uint32_t tp = 0;
+            for (uint32_t i = 0; i < kPlanThreads / 64; ++i) {
+                to += s_o[i];
+                tp += s_p[i];
+            }
+            s_carry_o += to;
+            s_carry_p += tp;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        B.out_off[B.nblobs] = s_carry_o;
+        B.piece_base[B.nblobs] = s_carry_p;
+        B.status[0] = s_carry_o > B.out_cap ? uint64_t(uint32_t(CDC_E_NOSPACE)) : 0ull;
+    }
 }
 
 // Where the LZ4 stages write blob b's frame: the frame buffer when it is
@@ -917,6 +1009,17 @@ static int ensure_tables()
 
 static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// Workspace kept per device between calls (grow-only); a call holds its
+// device's lock while it runs (the entry point is synchronous).
+struct WsCache {
+    std::mutex mu;
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    hipStream_t aux = nullptr;  // k_xxh32 runs here, beside the LZ4 and GCM kernels
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static WsCache g_ws[64];
+
 }  // namespace enc
 
 using namespace enc;
@@ -979,8 +1082,21 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     const size_t o_bsz = take(nk * 4), o_bfo = take(nk * 8), o_xxh = take(nb * 4), o_flen = take(nb * 8);
     const size_t o_oo = take((nb + 1) * 8), o_pb = take((nb + 1) * 4), o_keys = take(encrypt ? nb * sizeof(BlobKey) : 0);
     const size_t o_status = take(8), o_frames = take(encrypt ? slot : 0);
-    uint8_t *ws = nullptr;
-    if (hipMalloc(&ws, off ? off : 16) != hipSuccess) return CDC_E_DEVICE;
+    if (device < 0 || device >= 64) return CDC_E_INVALID;
+    WsCache &C = g_ws[device];
+    std::lock_guard<std::mutex> lk(C.mu);
+    if (C.cap < off) {
+        if (C.p) (void)hipFree(C.p);
+        C.p = nullptr;
+        C.cap = 0;
+        if (hipMalloc(&C.p, off) != hipSuccess) return CDC_E_DEVICE;
+        C.cap = off;
+    }
+    uint8_t *ws = C.p;
+    if (!C.aux && (hipStreamCreateWithFlags(&C.aux, hipStreamNonBlocking) != hipSuccess ||
+                   hipEventCreateWithFlags(&C.fork, hipEventDisableTiming) != hipSuccess ||
+                   hipEventCreateWithFlags(&C.join, hipEventDisableTiming) != hipSuccess))
+        return CDC_E_DEVICE;
     Batch Bt{};
     Bt.base = static_cast<const uint8_t *>(d_base);
     Bt.nblobs = n;
@@ -1021,14 +1137,17 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     }
     if (ok && n) {
         if (compress) {
-            hipLaunchKernelGGL(k_xxh32, dim3((n + 3) / 4), dim3(256), 0, s, Bt);
+            ok = hipEventRecord(C.fork, s) == hipSuccess && hipStreamWaitEvent(C.aux, C.fork, 0) == hipSuccess;
+            hipLaunchKernelGGL(k_xxh32, dim3((n + kXxWaves - 1) / kXxWaves), dim3(kXxWaves * 64), 0, C.aux, Bt);
+            ok = ok && hipEventRecord(C.join, C.aux) == hipSuccess;
             if (ng) hipLaunchKernelGGL(k_lz4_seq, dim3(uint32_t((ng + kSeqWaves - 1) / kSeqWaves)), dim3(kSeqWaves * 64), 0, s, Bt);
             if (nk) hipLaunchKernelGGL(k_lz4_size, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
         }
-        hipLaunchKernelGGL(k_enc_plan, dim3(1), dim3(64), 0, s, Bt);
+        hipLaunchKernelGGL(k_enc_plan, dim3(1), dim3(kPlanThreads), 0, s, Bt);
         if (encrypt) hipLaunchKernelGGL(k_blob_keys, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
         if (compress) {
             if (nk) hipLaunchKernelGGL(k_lz4_emit, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
+            ok = ok && hipStreamWaitEvent(s, C.join, 0) == hipSuccess;  // the content checksums
             hipLaunchKernelGGL(k_frame_fin, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
         } else if (!encrypt) {
             hipLaunchKernelGGL(k_copy, dim3(n), dim3(256), 0, s, Bt);
@@ -1047,7 +1166,6 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
         }
         ok = ok && hipStreamSynchronize(s) == hipSuccess;
     }
-    (void)hipFree(ws);
     if (!ok) return CDC_E_DEVICE;
     return status ? int(int32_t(uint32_t(status))) : CDC_OK;
 }

@@ -60,3 +60,23 @@ def encode_blobs(blobs, key=None, compress=True, random=None, device=0):
     oo = encode_device(base, offs[:-1], lens, out, key=key, compress=compress, random=random, device=device)
     host = out[:oo[-1]].cpu().numpy()
     return [host[oo[i]:oo[i + 1]].tobytes() for i in range(len(lens))]
+
+
+class DeviceEncoder:
+    """(*Repository).Encode with the repository's configuration: compression
+    "LZ4" (compression.DefaultConfiguration) or None, and the encryption key
+    (None: no encryption).  `encode_many` encodes a whole batch of blobs in
+    one device call; calling the object encodes one blob, like Encode."""
+
+    def __init__(self, key=None, compression="LZ4", device=0):
+        if compression not in (None, "LZ4"):
+            raise ValueError(f"unsupported compression {compression!r} (the device path implements LZ4)")
+        self.key = None if key is None else bytes(key)
+        self.compress = compression == "LZ4"
+        self.device = device
+
+    def encode_many(self, blobs):
+        return encode_blobs(blobs, key=self.key, compress=self.compress, device=self.device)
+
+    def __call__(self, blob):
+        return self.encode_many([blob])[0]

@@ -172,7 +172,9 @@ def backup_batch(files, repo: Repository = None, known=None, max_size=None, enco
     known: set of chunk checksums already stored (BlobExists); updated.
     encode: Repository.Encode (compression, then encryption:
     repository/repository.go:212-236) applied to each blob before it is
-    packed, as PutBlob does; None = no compression / no encryption.
+    packed, as PutBlob does: a callable per blob, or an
+    encode.DeviceEncoder (all new blobs of the batch in one device call);
+    None = no compression / no encryption.
     Returns (objects, packfiles): the Object records and the serialised
     packfiles (packfile.go Serialize form)."""
     from . import packer as packer_mod
@@ -194,6 +196,25 @@ def backup_batch(files, repo: Repository = None, known=None, max_size=None, enco
         return objects, packs
     packs = []
     pk = packer_mod.Packer(max_size, timestamp)
+    if hasattr(encode, "encode_many"):  # encode.DeviceEncoder: every new blob of the batch in one device call
+        todo = []
+        for a, obj in zip(arrs, objects):
+            off = 0
+            for c in obj.Chunks:
+                data = a[off:off + c.Length]
+                off += c.Length
+                if c.Checksum in known:
+                    continue
+                known.add(c.Checksum)
+                todo.append((c.Checksum, data))
+        for (csum, _), enc in zip(todo, encode.encode_many([d for _, d in todo])):
+            if pk.AddBlob(packer_mod.TYPE_CHUNK, csum, enc):
+                packs.append(pk.Serialize())
+                pk.Reset()
+        if pk.Count():
+            packs.append(pk.Serialize())
+        pk.close()
+        return objects, packs
     for a, obj in zip(arrs, objects):
         off = 0
         for c in obj.Chunks:

@@ -150,3 +150,25 @@ def test_encode_device_resident_batch():
     small = torch.empty(oo[-1] - 1, dtype=torch.uint8, device="cuda")
     with pytest.raises(_lib.CdcError):
         encode.encode_device(t, offs, lens, small, key=KEY)
+
+
+def test_backup_batch_device_encoder():
+    """backup_batch with the device Encode: every blob in the packfiles opens
+    under the repository key and inflates to its chunk (Decode, then the
+    chunk's SHA-256 is its index checksum)."""
+    import hashlib
+
+    import packfile_ref as pf
+    from plakar_amd import snapshot
+    files = [low_entropy(n, 80 + i) for i, n in enumerate([0, 5000, 70_000, 6 << 20, 13 << 20])]
+    files.append(random_bytes(3 << 20, 90))
+    enc = encode.DeviceEncoder(key=KEY)
+    objs, packs = snapshot.backup_batch(files, known=set(), max_size=4 << 20, encode=enc, timestamp=7)
+    seen = 0
+    for pk in packs:
+        p = pf.parse(pk)
+        for t, c, o, n in p.index:
+            plain = ref.decode(bytes(p.blobs[o:o + n]), key=KEY)
+            assert hashlib.sha256(plain).digest() == c
+            seen += 1
+    assert seen == len({c.Checksum for ob in objs for c in ob.Chunks})
