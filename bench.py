@@ -183,6 +183,90 @@ def digest_leg(torch, batch, bufs, reps, check):
     return d
 
 
+def _cpu_encode_rate(host, cuts, seconds=3.0):
+    """CPU baseline of Encode on one host core: LZ4 frames (the system's
+    liblz4, LZ4F_compressFrame) then AES-256-GCM over 64-KiB pieces (OpenSSL
+    libcrypto), chunk by chunk over a bounded sample; None without the libraries."""
+    import ctypes
+    import ctypes.util
+    try:
+        lz = ctypes.CDLL(ctypes.util.find_library("lz4") or "liblz4.so.1")
+        cr = ctypes.CDLL(ctypes.util.find_library("crypto") or "libcrypto.so.3")
+    except OSError:
+        return None
+    lz.LZ4F_compressFrameBound.restype = ctypes.c_size_t
+    lz.LZ4F_compressFrameBound.argtypes = [ctypes.c_size_t, ctypes.c_void_p]
+    lz.LZ4F_compressFrame.restype = ctypes.c_size_t
+    lz.LZ4F_compressFrame.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    cr.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
+    cr.EVP_aes_256_gcm.restype = ctypes.c_void_p
+    cr.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+    cr.EVP_EncryptUpdate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p,
+                                     ctypes.c_int]
+    cr.EVP_EncryptFinal_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    cr.EVP_CIPHER_CTX_ctrl.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    cr.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
+    key, nonce = os.urandom(32), os.urandom(12)
+    dst = ctypes.create_string_buffer(int(lz.LZ4F_compressFrameBound(4 << 20, None)) + 64)
+    enc = ctypes.create_string_buffer((4 << 20) + 4096)
+    tag = ctypes.create_string_buffer(16)
+    ol = ctypes.c_int()
+    nbytes, t0 = 0, time.perf_counter()
+    for o, n in cuts:
+        src = host[int(o):int(o + n)]
+        m = lz.LZ4F_compressFrame(dst, len(dst), src.ctypes.data, int(n), None)
+        for p0 in range(0, int(m), 65536):
+            ctx = cr.EVP_CIPHER_CTX_new()
+            cr.EVP_EncryptInit_ex(ctx, cr.EVP_aes_256_gcm(), None, key, nonce)
+            cr.EVP_EncryptUpdate(ctx, enc, ctypes.byref(ol), ctypes.addressof(dst) + p0, min(65536, int(m) - p0))
+            cr.EVP_EncryptFinal_ex(ctx, enc, ctypes.byref(ol))
+            cr.EVP_CIPHER_CTX_ctrl(ctx, 0x10, 16, tag)
+            cr.EVP_CIPHER_CTX_free(ctx)
+        nbytes += int(n)
+        if time.perf_counter() - t0 > seconds:
+            break
+    el = time.perf_counter() - t0
+    return dict(value=round(nbytes / el / GIB, 3), unit="GiB/s", cores=1, kind="liblz4 + OpenSSL AES-256-GCM",
+                sample=f"{nbytes >> 20} MiB of chunks of buffer 0, LZ4F_compressFrame then GCM per 64-KiB piece, 1 thread")
+
+
+def encode_leg(torch, batch, bufs, reps, baseline):
+    """Encode (LZ4 frame + AES-256-GCM stream, repository/repository.go:212-236)
+    of every chunk of the pass, device-resident, with a random key; GiB/s of
+    chunk bytes, the encoded/raw ratio, and a 1-core CPU baseline.  Not part
+    of `value`."""
+    import numpy as np
+    from plakar_amd import encode
+    key = os.urandom(32)
+    cuts, _ = batch.results()
+    plans = []
+    for t, c in zip(bufs, cuts):
+        c = c.cpu().numpy().astype(np.int64)
+        lens = c[:, 1].tolist()
+        cap = sum(encode.encode_bound(x) for x in lens)
+        plans.append((t, c[:, 0].tolist(), lens, torch.empty(max(cap, 1), dtype=torch.uint8, device=t.device)))
+    encoded = 0
+    for t, offs, lens, out in plans:  # warm
+        encoded += encode.encode_device(t, offs, lens, out, key=key)[-1]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for t, offs, lens, out in plans:
+            encode.encode_device(t, offs, lens, out, key=key)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    total = sum(t.numel() for t in bufs)
+    d = dict(value=round(total / el / GIB, 2), unit="GiB/s", ms_per_pass=round(el * 1e3, 3),
+             ratio=round(encoded / max(total, 1), 4), blobs=sum(len(p[2]) for p in plans),
+             kernels="k_xxh32 (side stream), k_lz4_seq, k_lz4_size, k_enc_plan, k_lz4_emit, k_frame_fin, k_blob_keys, k_gcm",
+             note="wall time per pass incl. the host plan (segment/block tables) and its upload")
+    if baseline:
+        host = bufs[0][:min(bufs[0].numel(), 256 << 20)].cpu().numpy()
+        c0 = [(o, n) for o, n in zip(plans[0][1], plans[0][2]) if o + n <= host.size]
+        d["cpu_baseline"] = _cpu_encode_rate(host, c0)
+    return d
+
+
 def chunk_digest_pipeline(torch, bufs, opts, dev, nstreams, passes):
     """Chunking + per-chunk SHA-256 and histograms (processChunk's device work,
     snapshot/backup.go:594-629) as a backup streams batches: each pass chunks
@@ -289,6 +373,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="device workloads: consecutive steps alternate over this many streams, each with its "
                          "own workspace, so one batch's resolution kernels overlap the next batch's scan")
+    ap.add_argument("--encode-reps", type=int, default=3,
+                    help="Encode leg (LZ4 frame + AES-256-GCM of every chunk, not part of value); 0 disables")
     ap.add_argument("--digest-reps", type=int, default=3,
                     help="reps of the per-chunk SHA-256 + histogram leg (SURVEY.md 8f; 0 = skip)")
     ap.add_argument("--digest-streams", type=int, default=4,
@@ -442,6 +528,10 @@ def main():
         digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_streams,
                                                                   max(args.digest_streams * 2, 8))
 
+    encode_res = None
+    if not host_mode and args.encode_reps > 0:
+        encode_res = encode_leg(torch, batch, bufs, args.encode_reps, rank == 0 and world == 1)
+
     baseline, parity, e2e = None, None, None
     if rank == 0 and world == 1:
         import numpy as np
@@ -499,6 +589,7 @@ def main():
             "parity_vs_oracle": parity,
             "e2e_host_path": e2e,
             "chunk_digests": digest,
+            "encode": encode_res,
         }
         print(json.dumps(line), flush=True)
     if host_mode and wl.get("files"):

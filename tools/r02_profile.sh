@@ -10,7 +10,7 @@ QUICK=${2:-}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-SHORT="--steps 3 --warmup 1 --streams 1 --no-cpu-baseline --e2e-reps 0 --digest-reps 0"
+SHORT="--steps 3 --warmup 1 --streams 1 --no-cpu-baseline --e2e-reps 0 --digest-reps 0 --encode-reps 0"
 
 if [ -z "$QUICK" ]; then
     echo "[1] pytest -m gpu"
