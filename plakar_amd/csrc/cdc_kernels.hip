@@ -1824,7 +1824,8 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B,
 // ---------------------------------------------------------------------------
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-uint64_t align_tasks(uint64_t t) { return (t + kS2Waves - 1) / kS2Waves * kS2Waves; }
+// Scan tasks of one buffer (a workgroup's waves may belong to different buffers).
+uint64_t align_tasks(uint64_t t) { return t; }
 
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 {
@@ -1846,7 +1847,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     seg = (seg + 15) & ~15ull;
     plan->seg = seg;
     // Scan lane length: one scan workgroup per CU (a workgroup holds 112 KiB of
-    // LDS), for a target grid of one workgroup per CU; lane lengths are
+    // LDS), for a grid of at most CUs - 7 workgroups; lane lengths are
     // multiples of 256 B (odd multiples of 128 B ran slower), so 1 GiB takes
     // 249 workgroups of 5,632-B lanes.  Against CUs - 8 (238 workgroups) that
     // is +2.8 % pipelined from a cold start and +1 % for the isolated scan
@@ -1861,7 +1862,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
             n = 256;
         return uint64_t(n);
     }();
-    uint64_t wgs = cus;
+    uint64_t wgs = cus > 16 ? cus - 7 : cus;
     if (const char *env = getenv("CDC_SCAN_WGS")) {
         const long v = atol(env);
         if (v >= 1 && v <= 65536) wgs = uint64_t(v);
@@ -1870,6 +1871,14 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     want = (want + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
     if (want < 512) want = (512 + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
     if (want > kScanLaneBytes) want = kScanLaneBytes / kLaneQuant * kLaneQuant;
+    // buffers split into tasks independently: lengthen the lane until the
+    // grid fits the target (a full 256-workgroup grid ran 7 % slower on C2)
+    auto grid_of = [&](uint64_t ln) {
+        uint64_t t = 0;
+        for (int i = 0; i < nbufs; ++i) t += (lens[i] + 64 * ln - 1) / (64 * ln);
+        return (t + kS2Waves - 1) / kS2Waves;
+    };
+    while (want + kLaneQuant <= kScanLaneBytes && grid_of(want) > wgs) want += kLaneQuant;
     uint32_t lane = uint32_t(want);
     if (const char *env = getenv("CDC_SCAN_LANE_BYTES")) {
         const long v = atol(env);

@@ -50,6 +50,9 @@ done
 cat "$OUT/pmc_c1_k_scan.txt"
 
 if [ -z "$QUICK" ]; then
+    echo "[5] bench c1 (default command: 200 warm-up + 200 timed passes, all legs)"
+    timeout -k 10 400 python3 bench.py > "$OUT/bench_c1.json" 2> "$OUT/bench_c1.err"
+    cut -c1-200 "$OUT/bench_c1.json"
     for wl in c2 c3; do
         echo "[5] bench $wl"
         timeout -k 10 200 python3 bench.py --workload $wl --no-cpu-baseline > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err"
