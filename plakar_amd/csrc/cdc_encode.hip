@@ -223,10 +223,24 @@ __device__ __forceinline__ G128 g_from_words(const uint32_t w[4])
 struct BlobKey {
     uint32_t rk[60];
     uint32_t pad[4];
-    G128 th[16];
-    G128 th64[16];
-    G128 hpow[64];
+    G128 th[16];      // 4-bit table of H (the length block)
+    G128 hpow[64];    // H^1 .. H^64
+    G128 t64[256];    // 8-bit table of H^64 (the lanes' Horner steps)
 };
+
+// 8-bit table: T[i] = i * V for the byte i read MSB-first (T[128] = V).
+__device__ void gtable8(G128 v, G128 *t)
+{
+    auto half = [](G128 x) {
+        const uint64_t r = (x.lo & 1) ? 0xE100000000000000ull : 0;
+        return G128{(x.hi >> 1) ^ r, (x.lo >> 1) | (x.hi << 63)};
+    };
+    t[0] = {0, 0};
+    t[128] = v;
+    for (int i = 64; i; i >>= 1) t[i] = half(t[2 * i]);
+    for (int i = 2; i < 256; i <<= 1)
+        for (int j = 1; j < i; ++j) t[i + j] = gx(t[i], t[j]);
+}
 
 struct Seg {             // a 16-KiB LZ4 search segment
     uint64_t src;        // byte offset in the input base
@@ -857,9 +871,7 @@ __global__ __launch_bounds__(64) void k_blob_keys(const Batch B)
         p = gmul4(p, th);
         K.hpow[e] = p;
     }
-    G128 t64[16];
-    gtable(p, t64);
-    for (int i = 0; i < 16; ++i) K.th64[i] = t64[i];
+    gtable8(p, K.t64);
     // header: subkey nonce || Seal(repository key, subkey nonce, subkey)
     uint8_t *o = B.out + B.out_off[b];
     for (int i = 0; i < 12; ++i) o[i] = r[32 + i];
@@ -872,24 +884,78 @@ __global__ __launch_bounds__(64) void k_blob_keys(const Batch B)
 
 constexpr uint32_t kGcmWaves = 4;
 
+// LDS of a GCM workgroup.  The T-table in 32 copies, entry e of copy c at word
+// 32 e + c: lane l reads copy l & 31, so the 32 lanes of a ds_read_b32 group
+// always hit 32 distinct banks whatever the state bytes (the S-box of the
+// last round is byte 2 of the same entry).  rem8: the reduction of the 8 bits
+// a GHASH step shifts out.
 struct GcmLds {
-    uint32_t te[256];
-    uint8_t sb[256];
+    uint32_t te[256 * 32];
+    uint64_t rem8[256];
     struct PerWave {
         uint32_t rk[60];
-        G128 th64[16];
         G128 th[16];
+        G128 t64[256];
+        uint4 stage[64];
     } w[kGcmWaves];
 };
+
+__device__ __forceinline__ void aes256_block_lds(const uint32_t *rk, const uint32_t *te, uint32_t c, uint32_t s[4])
+{
+    auto T = [&](uint32_t x) { return te[(x << 5) | c]; };
+    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t t0 = T(s0 >> 24) ^ ror32(T((s1 >> 16) & 255), 8) ^ ror32(T((s2 >> 8) & 255), 16) ^
+                            ror32(T(s3 & 255), 24) ^ rk[4 * r];
+        const uint32_t t1 = T(s1 >> 24) ^ ror32(T((s2 >> 16) & 255), 8) ^ ror32(T((s3 >> 8) & 255), 16) ^
+                            ror32(T(s0 & 255), 24) ^ rk[4 * r + 1];
+        const uint32_t t2 = T(s2 >> 24) ^ ror32(T((s3 >> 16) & 255), 8) ^ ror32(T((s0 >> 8) & 255), 16) ^
+                            ror32(T(s1 & 255), 24) ^ rk[4 * r + 2];
+        const uint32_t t3 = T(s3 >> 24) ^ ror32(T((s0 >> 16) & 255), 8) ^ ror32(T((s1 >> 8) & 255), 16) ^
+                            ror32(T(s2 & 255), 24) ^ rk[4 * r + 3];
+        s0 = t0;
+        s1 = t1;
+        s2 = t2;
+        s3 = t3;
+    }
+    auto S = [&](uint32_t x) { return (T(x) >> 16) & 255u; };
+    s[0] = (S(s0 >> 24) << 24 | S((s1 >> 16) & 255) << 16 | S((s2 >> 8) & 255) << 8 | S(s3 & 255)) ^ rk[56];
+    s[1] = (S(s1 >> 24) << 24 | S((s2 >> 16) & 255) << 16 | S((s3 >> 8) & 255) << 8 | S(s0 & 255)) ^ rk[57];
+    s[2] = (S(s2 >> 24) << 24 | S((s3 >> 16) & 255) << 16 | S((s0 >> 8) & 255) << 8 | S(s1 & 255)) ^ rk[58];
+    s[3] = (S(s3 >> 24) << 24 | S((s0 >> 16) & 255) << 16 | S((s1 >> 8) & 255) << 8 | S(s2 & 255)) ^ rk[59];
+}
+
+// x * V with V's 8-bit table (byte by byte from the last).
+__device__ __forceinline__ G128 gmul8(G128 x, const G128 *t, const uint64_t *rem8)
+{
+    G128 z = t[uint32_t(x.lo) & 255u];
+#pragma unroll
+    for (int i = 14; i >= 0; --i) {
+        const uint32_t byte = i >= 8 ? uint32_t(x.lo >> (8 * (15 - i))) & 255u : uint32_t(x.hi >> (8 * (7 - i))) & 255u;
+        const uint32_t rem = uint32_t(z.lo) & 255u;
+        z.lo = (z.hi << 56) | (z.lo >> 8);
+        z.hi = (z.hi >> 8) ^ rem8[rem];
+        const G128 e = t[byte];
+        z.hi ^= e.hi;
+        z.lo ^= e.lo;
+    }
+    return z;
+}
+
+__device__ __forceinline__ uint32_t be32(uint32_t x) { return __builtin_bswap32(x); }
 
 __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
 {
     __shared__ GcmLds L;
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-        L.te[i] = g_te0[i];
-        L.sb[i] = g_sbox[i];
+    for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) L.te[i] = g_te0[i >> 5];
+    for (uint32_t r = threadIdx.x; r < 256; r += blockDim.x) {
+        uint64_t x = 0;
+        for (uint32_t b = 0; b < 8; ++b)
+            if (r & (1u << b)) x ^= uint64_t(0xE100u >> (7 - b));
+        L.rem8[r] = x << 48;
     }
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, cpy = lane & 31u;
     const uint32_t pc = blockIdx.x * kGcmWaves + wv;
     const uint32_t total = B.piece_base[B.nblobs];
     const bool active = pc < total && !B.status[0];
@@ -904,10 +970,8 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         b = lo;
         const BlobKey &K = B.keys[b];
         for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk[i] = K.rk[i];
-        if (lane < 16) {
-            L.w[wv].th64[lane] = K.th64[lane];
-            L.w[wv].th[lane] = K.th[lane];
-        }
+        if (lane < 16) L.w[wv].th[lane] = K.th[lane];
+        for (uint32_t i = lane; i < 256; i += 64) L.w[wv].t64[i] = K.t64[i];
     }
     __syncthreads();
     if (!active) return;
@@ -918,6 +982,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint32_t m = uint32_t(min<uint64_t>(kPiece, F - p0));  // piece bytes
     const uint32_t nb = (m + 15) / 16;
     const uint8_t *pt = plain_ptr(B, b) + p0;
+    const bool pt_al = (reinterpret_cast<uintptr_t>(pt) & 15u) == 0;
     uint8_t *o = B.out + B.out_off[b] + 60 + uint64_t(k) * (kPiece + 28);
     const uint8_t *dn = B.rnd + 56ull * b + 44;  // data nonce
     uint32_t j0[3];
@@ -927,35 +992,53 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     if (lane < 12) o[lane] = uint8_t(j0[lane >> 2] >> (24 - 8 * (lane & 3)));
     uint8_t *ct = o + 12;
     const uint32_t *rk = L.w[wv].rk;
-    // lane: blocks lane, lane + 64, ...; Horner in H^64
+    const G128 *t64 = L.w[wv].t64;
+    uint8_t *stage = reinterpret_cast<uint8_t *>(L.w[wv].stage);
+    // row j: blocks 64 j + lane (1 KiB of the piece); lane: Horner in H^64 over its blocks
     G128 Z = {0, 0};
     uint32_t cnt = 0;
-    for (uint32_t i = lane; i < nb; i += 64) {
-        uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
-        aes256_block(rk, L.te, L.sb, c);
-        const uint32_t bytes = min(16u, m - 16 * i);
-        uint8_t blk[16];
-        for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
-        uint32_t w[4];
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t pw = uint32_t(blk[4 * q]) << 24 | uint32_t(blk[4 * q + 1]) << 16 |
-                                uint32_t(blk[4 * q + 2]) << 8 | blk[4 * q + 3];
-            w[q] = c[q] ^ pw;
+    const uint32_t rows = (nb + 63) / 64;
+    for (uint32_t j = 0; j < rows; ++j) {
+        const uint32_t i = 64 * j + lane;
+        uint4 cw = make_uint4(0, 0, 0, 0);
+        if (i < nb) {
+            uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
+            aes256_block_lds(rk, L.te, cpy, c);
+            const uint32_t bytes = min(16u, m - 16 * i);
+            uint32_t pw[4];
+            if (pt_al && bytes == 16) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(pt + 16 * i);
+                pw[0] = be32(v.x);
+                pw[1] = be32(v.y);
+                pw[2] = be32(v.z);
+                pw[3] = be32(v.w);
+            } else {
+                uint8_t blk[16];
+                for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
+                gcm_block_words(blk, pw);
+            }
+            uint32_t w[4];
+            for (int q = 0; q < 4; ++q) w[q] = c[q] ^ pw[q];
+            if (bytes < 16) {  // the keystream past the piece's end is not ciphertext (nor hashed)
+                for (int q = 0; q < 4; ++q) {
+                    const int keep = int(bytes) - 4 * q;
+                    w[q] = keep >= 4 ? w[q] : keep <= 0 ? 0u : (w[q] & ~(0xFFFFFFFFu >> (8 * keep)));
+                }
+            }
+            cw = make_uint4(be32(w[0]), be32(w[1]), be32(w[2]), be32(w[3]));
+            Z = gx(gmul8(Z, t64, L.rem8), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
+            ++cnt;
         }
-        uint8_t cb[16];
-        for (int q = 0; q < 4; ++q) {
-            cb[4 * q] = uint8_t(w[q] >> 24);
-            cb[4 * q + 1] = uint8_t(w[q] >> 16);
-            cb[4 * q + 2] = uint8_t(w[q] >> 8);
-            cb[4 * q + 3] = uint8_t(w[q]);
+        // the row's ciphertext through LDS: 16 coalesced byte stores of 64 bytes
+        L.w[wv].stage[lane] = cw;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t row_bytes = min(1024u, m - 1024 * j);
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q) {
+            const uint32_t x = 64 * q + lane;
+            if (x < row_bytes) ct[1024 * j + x] = stage[x];
         }
-        for (uint32_t q = 0; q < bytes; ++q) ct[16 * i + q] = cb[q];
-        if (bytes < 16)
-            for (uint32_t q = bytes; q < 16; ++q) cb[q] = 0;
-        uint32_t cw[4];
-        gcm_block_words(cb, cw);
-        Z = gx(gmul4(Z, L.w[wv].th64), g_from_words(cw));
-        ++cnt;
+        __builtin_amdgcn_wave_barrier();
     }
     if (cnt) {
         const uint32_t e = nb - lane - 64 * (cnt - 1);  // 1..64
@@ -968,7 +1051,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     if (lane == 0) {
         G128 S = gmul4(gx(Z, G128{0, uint64_t(m) * 8}), L.w[wv].th);
         uint32_t t[4] = {j0[0], j0[1], j0[2], 1};
-        aes256_block(rk, L.te, L.sb, t);
+        aes256_block_lds(rk, L.te, cpy, t);
         const uint64_t hi = S.hi ^ (uint64_t(t[0]) << 32 | t[1]), lo = S.lo ^ (uint64_t(t[2]) << 32 | t[3]);
         uint8_t *tag = ct + m;
         for (int q = 0; q < 8; ++q) {

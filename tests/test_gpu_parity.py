@@ -366,6 +366,24 @@ def test_chunker_next_mirror(oracle):
     assert chk.Next() == (None, chunkers.EOF)
 
 
+@pytest.mark.parametrize("window_mib,size_mib", [(200, 93), (200, 199)])
+def test_chunker_large_window_final_fill(oracle, window_mib, size_mib):
+    """A stream through an explicit 200-MiB window whose final fill is shorter
+    than the window: the plan of the shorter fill can need more workspace than
+    the window's (the scan lane rounds up), and the stream regrows it."""
+    _lib.ensure_init()
+    data = random_bytes((size_mib << 20) + 12345, 97 + size_mib)
+    chk = chunkers.NewChunker("fastcdc", io.BytesIO(data.tobytes()), _opts(DEF), window_bytes=window_mib << 20)
+    lens = []
+    while True:
+        chunk, err = chk.Next()
+        if err is chunkers.EOF:
+            break
+        lens.append(len(chunk))
+    ref = oracle.chunk(data, _placeholder(), **DEF)
+    assert lens == [int(x) for x in ref[:, 1]]
+
+
 def test_chunker_rejects_like_go():
     _lib.ensure_init()
     with pytest.raises(_lib.CdcError):
