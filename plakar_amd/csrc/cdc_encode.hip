@@ -8,23 +8,25 @@
 // compressed stream sealed under the subkey with its own nonce.
 //
 // Kernels, in launch order (one batch = the blobs of one call):
-//   k_xxh32       one wave per blob: XXH32 of the blob (the frame's content
-//                 checksum), its four accumulators on lanes 0-3
-//   k_lz4_seq     one wave per 16-KiB segment: greedy LZ4 match search over a
-//                 64-position window per step (hash table of 4,096 u16 in LDS,
-//                 matches found by ballot, extended 64 bytes per step);
-//                 sequences out as (match start, offset, length) records
+//   k_xxh32       XXH32 of every blob (the frame's content checksum), on a
+//                 side stream: four blobs per wave, a lane quad's chains each
+//   k_lz4_seq     one wave per 16-KiB segment: greedy LZ4 match search, 64
+//                 positions per step at LZ4's accelerating stride (hash table
+//                 of 4,096 u16 in LDS, matches found by ballot, extended 64
+//                 bytes per step both ways); sequences out as (match start,
+//                 offset, length) records
 //   k_lz4_size    one workgroup per 4-MiB LZ4 block: literal runs across
 //                 segment boundaries, encoded size (raw when not smaller)
 //   k_enc_plan    one workgroup: frame sizes, block offsets in the frame,
 //                 GCM pieces and output offsets of every blob (scans)
-//   k_lz4_emit    one workgroup per block: the block's bytes in the frame
+//   k_lz4_emit    a workgroup per block (16 per stored block): its bytes
 //   k_frame_fin   one wave per blob: frame header, end mark, checksum
 //   k_blob_keys   one lane per blob: the subkey's round keys, H and its
 //                 powers H^1..H^64, and the sealed subkey (header)
-//   k_gcm         one wave per 64-KiB piece: AES-256-CTR (T-table in LDS)
-//                 and GHASH (4-bit tables: lane l hashes blocks l, l+64, ...
-//                 by Horner in H^64, then multiplies by its own H^e), tag
+//   k_gcm         one wave per 64-KiB piece: AES-256-CTR (T-table in LDS,
+//                 32 bank-conflict-free copies) and GHASH (lane l hashes
+//                 blocks l, l+64, ... by Horner in H^64 with an 8-bit table,
+//                 then multiplies by its own H^e), tag
 //
 // Matches stay inside their 16-KiB segment, so compression ratios are those
 // of LZ4 with a 16-KiB window; any LZ4 decoder reads the frames (the tests
@@ -34,6 +36,7 @@
 // four bytes XOR k (big-endian), unique per subkey.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -287,9 +290,15 @@ struct Batch {
     uint32_t *piece_base;     // nblobs + 1
     BlobKey *keys;            // per blob
     uint64_t *status;         // [0]: CDC_E_NOSPACE when out_cap is too small
+    const uint32_t *xx_ids;   // XXH32 order of the blobs
 };
 
 constexpr uint32_t kNoneU32 = 0xFFFFFFFFu;
+
+// Global-memory views (global_load, counted in vmcnt only; a generic pointer
+// gives flat loads, which also count in lgkmcnt).
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+typedef __attribute__((address_space(1))) const uint8_t gu8;
 
 __device__ __forceinline__ uint32_t ld32u(const uint8_t *p)  // unaligned
 {
@@ -302,72 +311,28 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t *p)  // unaligned
 // ---------------------------------------------------------------------------
 constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u, P5 = 374761393u;
 
-// The stripes stream through LDS 4 KiB at a time (double-buffered: the whole
-// wave loads region r + 1 while lanes 0-3 run their chains over region r), so
-// the accumulators' dependent multiply chain, not memory latency, sets the pace.
+// A wave hashes kXxPerWave blobs (sorted longest first on the host: the
+// longest chains start first).  Their stripes stream through LDS, a region of
+// kXxRegion / kXxPerWave bytes per blob at a time, regions r + 1 and r + 2 in
+// flight while lane quad g runs blob g's four accumulator chains (lane a:
+// accumulator a) over region r.  The loading lanes store each word already
+// multiplied by PRIME32_2, so a chain step is add, rotate, multiply.  A batch
+// takes as long as its longest blob's chain (a 4-MiB blob: 262,144 steps);
+// more blobs per wave (less idle VALU work) measured slower, because the chain
+// latency, not VALU throughput, bounds it.
 constexpr uint32_t kXxWaves = 4;
-constexpr uint32_t kXxRegion = 4096;
+constexpr uint32_t kXxRegion = 4096;                 // bytes per wave per stage
+constexpr uint32_t kXxPerWave = 1;                   // blobs per wave
+constexpr uint32_t kXxBlobRegion = kXxRegion / kXxPerWave;
+constexpr uint32_t kXxLoadLanes = 64 / kXxPerWave;  // lanes loading one blob's region
+static_assert(kXxBlobRegion == 16 * 4 * kXxLoadLanes, "16 words per loading lane");
 
-__global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
+// The merge of the four accumulators, the tail and the avalanche.
+__device__ uint32_t xxh_finish(uint32_t v1, uint32_t v2, uint32_t v3, uint32_t v4, const uint8_t *p, uint64_t n)
 {
-    __shared__ uint32_t s_buf[kXxWaves][2][kXxRegion / 4];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kXxWaves + wv;
-    if (w >= B.nblobs) return;
-    const BlobDesc D = B.blobs[w];
-    const uint8_t *p = B.base + D.src;
-    const uint64_t n = D.len, stripes = n / 16, nwords = stripes * 4;
-    const uint32_t *A = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
-    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u) * 8u;
-    const uint64_t R = (stripes * 16 + kXxRegion - 1) / kXxRegion;
-    uint32_t pw[16];
-    auto prefetch = [&](uint64_t r) {
-#pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) {
-            const uint64_t k = r * (kXxRegion / 4) + 16 * lane + i;  // blob word
-            uint32_t x = 0;
-            if (k < nwords) {
-                x = A[k];
-                // misaligned: the next aligned word holds the word's last bytes (never past them)
-                if (sh) x = __builtin_amdgcn_alignbit(A[k + 1], x, sh);
-            }
-            pw[i] = x;
-        }
-    };
-    auto store = [&](uint64_t r) {
-#pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) s_buf[wv][r & 1][16 * lane + i] = pw[i];
-    };
-    uint32_t v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0u : 0u - P1;
-    if (R) {
-        prefetch(0);
-        store(0);
-    }
-    for (uint64_t r = 0; r < R; ++r) {
-        if (r + 1 < R) prefetch(r + 1);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): region r is in LDS
-        __builtin_amdgcn_wave_barrier();
-        if (lane < 4) {
-            const uint32_t *bw = s_buf[wv][r & 1];
-            const uint32_t ns = uint32_t(min<uint64_t>(kXxRegion / 16, stripes - r * (kXxRegion / 16)));
-            uint32_t s = 0;
-            for (; s + 8 <= ns; s += 8) {
-                uint32_t in[8];
-#pragma unroll
-                for (uint32_t j = 0; j < 8; ++j) in[j] = bw[4 * (s + j) + lane];
-#pragma unroll
-                for (uint32_t j = 0; j < 8; ++j) v = rol32(v + in[j] * P2, 13) * P1;
-            }
-            for (; s < ns; ++s) v = rol32(v + bw[4 * s + lane] * P2, 13) * P1;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (r + 1 < R) store(r + 1);
-    }
-    const uint32_t v1 = __shfl(v, 0), v2 = __shfl(v, 1), v3 = __shfl(v, 2), v4 = __shfl(v, 3);
-    if (lane != 0) return;
     uint32_t h = n >= 16 ? rol32(v1, 1) + rol32(v2, 7) + rol32(v3, 12) + rol32(v4, 18) : P5;
     h += uint32_t(n);
-    uint64_t i = stripes * 16;
+    uint64_t i = n / 16 * 16;
     for (; i + 4 <= n; i += 4) h = rol32(h + ld32u(p + i) * P3, 17) * P4;
     for (; i < n; ++i) h = rol32(h + p[i] * P5, 11) * P1;
     h ^= h >> 15;
@@ -375,7 +340,108 @@ __global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
     h ^= h >> 13;
     h *= P3;
     h ^= h >> 16;
-    B.xxh[w] = h;
+    return h;
+}
+
+__global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
+{
+    __shared__ uint32_t s_buf[kXxWaves][2][kXxRegion / 4];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t i0 = (blockIdx.x * kXxWaves + wv) * kXxPerWave;  // the wave's first blob (sorted order)
+    if (i0 >= B.nblobs) return;
+    // the blob this lane loads for (lg) and, for lanes < 4 kXxPerWave, chains (cg)
+    const uint32_t lg = lane / kXxLoadLanes, sub = lane % kXxLoadLanes, cg = lane >> 2, a = lane & 3u;
+    auto blob = [&](uint32_t g, const uint8_t *&p, uint64_t &n, uint32_t &w) {
+        const bool ok = i0 + g < B.nblobs;
+        w = ok ? B.xx_ids[i0 + g] : 0u;
+        p = B.base + (ok ? B.blobs[w].src : 0);
+        n = ok ? B.blobs[w].len : 0;
+    };
+    const uint8_t *lp, *cp;
+    uint64_t ln, cn;
+    uint32_t lw, cw;
+    blob(lg, lp, ln, lw);
+    blob(cg < kXxPerWave ? cg : 0u, cp, cn, cw);
+    const uint64_t lnw = ln / 16 * 4;  // words in the loaded blob's stripes
+    const uint64_t cstripes = cg < kXxPerWave ? cn / 16 : 0;
+    // a global-address-space pointer: flat loads would also count in
+    // lgkmcnt, so every LDS wait of the chains would wait for the prefetch too
+    const gu32 *A = reinterpret_cast<const gu32 *>(reinterpret_cast<uintptr_t>(lp) & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(lp) & 3u) * 8u;
+    // regions: the wave's longest blob (its first: sorted)
+    uint64_t n0;
+    {
+        const uint8_t *p0;
+        uint32_t w0;
+        blob(0, p0, n0, w0);
+    }
+    const uint64_t R = (n0 / 16 * 16 + kXxBlobRegion - 1) / kXxBlobRegion;
+    // regions r + 1 and r + 2 are in flight (register sets X and Y, taking
+    // turns) while the chains run over region r in LDS
+    uint32_t X[16], Y[16];
+    // Branch-free loads (a load under a lane condition makes the compiler wait
+    // for it before the branch joins, serialising the prefetch): indices are
+    // clamped to the blob's last aligned word.
+    // A misaligned word takes its last bytes from the next aligned word, which
+    // holds some of the blob's bytes; an aligned one ignores it (shift 0).
+    const uint64_t klast = ln ? ((reinterpret_cast<uintptr_t>(lp) & 3u) + ln - 1) / 4 : 0;
+    auto prefetch = [&](uint32_t (&pw)[16], uint64_t r) {
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) {
+            const uint64_t k = r * (kXxBlobRegion / 4) + 16 * sub + i;  // blob word
+            const uint64_t k0 = min(k, klast), k1 = min(k + 1, klast);
+            // the round's input product, off the chain (words past the stripes
+            // are loaded from the clamped index and never consumed)
+            pw[i] = __builtin_amdgcn_alignbit(A[k1], A[k0], sh) * P2;
+        }
+    };
+    auto store = [&](const uint32_t (&pw)[16], uint64_t r) {
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) s_buf[wv][r & 1][16 * lane + i] = pw[i];
+    };
+    uint32_t v = a == 0 ? P1 + P2 : a == 1 ? P2 : a == 2 ? 0u : 0u - P1;
+    auto chains = [&](uint64_t r) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): region r is in LDS
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t done = r * (kXxBlobRegion / 16);
+        if (cstripes > done) {
+            const uint32_t *bw = s_buf[wv][r & 1] + cg * (kXxBlobRegion / 4);
+            const uint32_t ns = uint32_t(min<uint64_t>(kXxBlobRegion / 16, cstripes - done));
+            uint32_t s = 0;
+            for (; s + 8 <= ns; s += 8) {
+                uint32_t in[8];
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) in[j] = bw[4 * (s + j) + a];
+#pragma unroll
+                for (uint32_t j = 0; j < 8; ++j) v = rol32(v + in[j], 13) * P1;
+            }
+            for (; s < ns; ++s) v = rol32(v + bw[4 * s + a], 13) * P1;
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    if (R) {
+        prefetch(X, 0);
+        store(X, 0);
+        prefetch(X, 1);
+        prefetch(Y, 2);
+    }
+    // step r: chains over r; region r + 1 (set of parity r) into LDS; its set loads r + 3
+    for (uint64_t r = 0; r < R; r += 2) {
+        chains(r);
+        if (r + 1 < R) {
+            store(X, r + 1);
+            prefetch(X, r + 3);
+            chains(r + 1);
+            if (r + 2 < R) {
+                store(Y, r + 2);
+                prefetch(Y, r + 4);
+            }
+        }
+    }
+    const uint32_t qb = lane & ~3u;
+    const uint32_t v1 = __shfl(v, int(qb)), v2 = __shfl(v, int(qb + 1)), v3 = __shfl(v, int(qb + 2)),
+                   v4 = __shfl(v, int(qb + 3));
+    if (a == 0 && cg < kXxPerWave && i0 + cg < B.nblobs) B.xxh[cw] = xxh_finish(v1, v2, v3, v4, cp, cn);
 }
 
 // ---------------------------------------------------------------------------
@@ -383,7 +449,8 @@ __global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
 // match length), segment-relative; the literals before a match are the bytes
 // since the previous match's end.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSeqWaves = 4;
+constexpr uint32_t kSeqWaves = 2;  // 24 KiB of LDS per wave: three workgroups per CU
+constexpr uint32_t kSkipShift = 6;  // LZ4's skip trigger
 
 struct SeqLds {
     uint32_t data[kSegLZ / 4 + 4];
@@ -435,7 +502,11 @@ __global__ __launch_bounds__(kSeqWaves * 64) void k_lz4_seq(const Batch B)
     uint2 *rec = B.recs + uint64_t(g) * kRecCap;
     uint32_t cursor = 0, anchor = 0, nrec = 0;
     while (cursor < start_lim) {
-        const uint32_t p = cursor + lane;
+        // LZ4's acceleration: the further from the last match, the sparser the
+        // positions tried (stride 1 + distance / 64), so incompressible data
+        // costs a few steps per segment
+        const uint32_t stride = 1u + ((cursor - anchor) >> kSkipShift);
+        const uint32_t p = cursor + lane * stride;
         const bool valid = p < start_lim;
         const uint32_t v = valid ? lds_rd32(L, p) : 0u;
         const uint32_t h = (v * 2654435761u) >> (32 - kHashBits);
@@ -446,13 +517,28 @@ __global__ __launch_bounds__(kSeqWaves * 64) void k_lz4_seq(const Batch B)
         __builtin_amdgcn_wave_barrier();
         if (!m) {
             if (valid) L.tab[h] = uint16_t(p + 1);
-            cursor += 64;
+            cursor += 64 * stride;
             continue;
         }
         const uint32_t f = uint32_t(__ffsll((unsigned long long)m) - 1);
-        const uint32_t q = cursor + f;
-        const uint32_t cq = uint32_t(__builtin_amdgcn_readlane(int(c), int(f)));
+        uint32_t q = cursor + f * stride;
+        uint32_t cq = uint32_t(__builtin_amdgcn_readlane(int(c), int(f)));
         uint32_t len = 4;
+        // extend backwards over the positions the stride skipped (not past the
+        // last match's end nor the candidate's segment start)
+        for (;;) {
+            const uint32_t room = min(q - anchor, cq);
+            if (!room) break;
+            const uint32_t k = lane + 1;
+            const bool eq = k <= room && lds_rd8(L, q - k) == lds_rd8(L, cq - k);
+            const uint64_t mm = __ballot(!eq);
+            const uint32_t run = mm ? uint32_t(__ffsll((unsigned long long)mm) - 1) : 64u;
+            const uint32_t back = min(run, room);
+            q -= back;
+            cq -= back;
+            len += back;
+            if (back < 64) break;
+        }
         for (;;) {
             const uint32_t i = q + len + lane;
             const bool eq = i < end_lim && lds_rd8(L, i) == lds_rd8(L, cq + len + lane);
@@ -470,6 +556,7 @@ __global__ __launch_bounds__(kSeqWaves * 64) void k_lz4_seq(const Batch B)
         // ones are looked up again from there and would only shadow older
         // candidates)
         if (valid && p < q + len) L.tab[h] = uint16_t(p + 1);
+        __builtin_amdgcn_wave_barrier();
         anchor = cursor = q + len;
     }
     if (lane == 0) {
@@ -676,17 +763,40 @@ __device__ __forceinline__ const uint8_t *plain_ptr(const Batch &B, uint32_t b)
     return B.compress ? B.frames + B.blobs[b].slot : B.base + B.blobs[b].src;
 }
 
+// dst[0, n) = src[0, n) by the threads [tid, nt): aligned dword stores, each
+// from two aligned source dwords (v_alignbit); the source's last aligned dword
+// is read whole, never past it.
+__device__ void copy_span(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t tid, uint32_t nt)
+{
+    const uint32_t head = uint32_t(min<uint64_t>(n, (4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u));
+    if (tid < head) dst[tid] = src[tid];
+    dst += head;
+    src += head;
+    n -= head;
+    const uint64_t nw = n / 4;
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst);
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(src) & 3u) * 8u;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
+    if (sh) {
+        for (uint64_t i = tid; i < nw; i += nt) dw[i] = __builtin_amdgcn_alignbit(sw[i + 1], sw[i], sh);
+    } else {
+        for (uint64_t i = tid; i < nw; i += nt) dw[i] = sw[i];
+    }
+    for (uint64_t i = 4 * nw + tid; i < n; i += nt) dst[i] = src[i];
+}
+
 // Neither compressed nor encrypted: the output is the blob (Encode with no
 // compression and no key configured).
 __global__ __launch_bounds__(256) void k_copy(const Batch B)
 {
     const uint32_t b = blockIdx.x;
     if (b >= B.nblobs || B.status[0]) return;
-    const uint8_t *src = B.base + B.blobs[b].src;
-    uint8_t *dst = B.out + B.out_off[b];
-    const uint64_t n = B.blobs[b].len;
-    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    copy_span(B.out + B.out_off[b], B.base + B.blobs[b].src, B.blobs[b].len, threadIdx.x, blockDim.x);
 }
+
+// Grid (blocks, kEmitSplit): a stored block is copied by all its kEmitSplit
+// workgroups, a compressed one written by the first.
+constexpr uint32_t kEmitSplit = 16;
 
 __global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
 {
@@ -696,17 +806,20 @@ __global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
     uint8_t *dst = frame_ptr(B, K.blob) + B.blk_foff[blockIdx.x];
     const uint8_t *src = B.base + K.src;
     const uint32_t bs = B.blk_size[blockIdx.x];
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && blockIdx.y == 0) {
         dst[0] = uint8_t(bs);
         dst[1] = uint8_t(bs >> 8);
         dst[2] = uint8_t(bs >> 16);
         dst[3] = uint8_t(bs >> 24);
     }
     dst += 4;
-    if (bs & 0x80000000u) {  // stored: the raw bytes
-        for (uint32_t i = threadIdx.x; i < K.len; i += kBlkThreads) dst[i] = src[i];
+    if (bs & 0x80000000u) {  // stored: the raw bytes, a slice per workgroup
+        const uint32_t a = uint32_t(uint64_t(K.len) * blockIdx.y / kEmitSplit);
+        const uint32_t e = uint32_t(uint64_t(K.len) * (blockIdx.y + 1) / kEmitSplit);
+        copy_span(dst + a, src + a, e - a, threadIdx.x, kBlkThreads);
         return;
     }
+    if (blockIdx.y) return;
     blk_prologue(B, K, L);
     const uint32_t nr = L.rbase[K.nseg];
     const uint32_t last_end = uint32_t(L.total);
@@ -981,8 +1094,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint64_t p0 = uint64_t(k) * kPiece;
     const uint32_t m = uint32_t(min<uint64_t>(kPiece, F - p0));  // piece bytes
     const uint32_t nb = (m + 15) / 16;
-    const uint8_t *pt = plain_ptr(B, b) + p0;
+    const gu8 *pt = reinterpret_cast<const gu8 *>(reinterpret_cast<uintptr_t>(plain_ptr(B, b) + p0));
     const bool pt_al = (reinterpret_cast<uintptr_t>(pt) & 15u) == 0;
+    const uint32_t pt_sh = uint32_t(reinterpret_cast<uintptr_t>(pt) & 3u);
     uint8_t *o = B.out + B.out_off[b] + 60 + uint64_t(k) * (kPiece + 28);
     const uint8_t *dn = B.rnd + 56ull * b + 44;  // data nonce
     uint32_t j0[3];
@@ -1007,11 +1121,15 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             const uint32_t bytes = min(16u, m - 16 * i);
             uint32_t pw[4];
             if (pt_al && bytes == 16) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(pt + 16 * i);
-                pw[0] = be32(v.x);
-                pw[1] = be32(v.y);
-                pw[2] = be32(v.z);
-                pw[3] = be32(v.w);
+                const gu32 *q = reinterpret_cast<const gu32 *>(pt + 16 * i);
+                for (int k = 0; k < 4; ++k) pw[k] = be32(q[k]);
+            } else if (bytes == 16) {  // aligned dwords + v_alignbit (the last one holds needed bytes)
+                const gu32 *aw = reinterpret_cast<const gu32 *>(reinterpret_cast<uintptr_t>(pt + 16 * i) & ~uintptr_t(3));
+                const uint32_t sh = pt_sh * 8u;
+                uint32_t x[5];
+                for (int q = 0; q < 4; ++q) x[q] = aw[q];
+                x[4] = sh ? aw[4] : 0u;
+                for (int q = 0; q < 4; ++q) pw[q] = be32(sh ? __builtin_amdgcn_alignbit(x[q + 1], x[q], sh) : x[q]);
             } else {
                 uint8_t blk[16];
                 for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
@@ -1151,6 +1269,9 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
         slot += align16(fmax);
         pieces_max += encrypt ? (fmax + kPiece - 1) / kPiece : 0;
     }
+    std::vector<uint32_t> xx_ids(n);  // XXH32 order: longest first (a wave's blobs end together)
+    for (uint32_t b = 0; b < n; ++b) xx_ids[b] = b;
+    std::stable_sort(xx_ids.begin(), xx_ids.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
     // one device allocation for the plan and the workspace
     const size_t nb = blobs.size(), nk = blks.size(), ng = segs.size();
     size_t off = 0;
@@ -1164,7 +1285,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     const size_t o_recs = take(ng * kRecCap * sizeof(uint2)), o_nrec = take(ng * 4), o_trail = take(ng * 4);
     const size_t o_bsz = take(nk * 4), o_bfo = take(nk * 8), o_xxh = take(nb * 4), o_flen = take(nb * 8);
     const size_t o_oo = take((nb + 1) * 8), o_pb = take((nb + 1) * 4), o_keys = take(encrypt ? nb * sizeof(BlobKey) : 0);
-    const size_t o_status = take(8), o_frames = take(encrypt ? slot : 0);
+    const size_t o_status = take(8), o_frames = take(encrypt ? slot : 0), o_xx = take(compress ? nb * 4 : 0);
     if (device < 0 || device >= 64) return CDC_E_INVALID;
     WsCache &C = g_ws[device];
     std::lock_guard<std::mutex> lk(C.mu);
@@ -1207,6 +1328,8 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     Bt.piece_base = reinterpret_cast<uint32_t *>(ws + o_pb);
     Bt.keys = reinterpret_cast<BlobKey *>(ws + o_keys);
     Bt.status = reinterpret_cast<uint64_t *>(ws + o_status);
+    Bt.xx_ids = reinterpret_cast<uint32_t *>(ws + o_xx);
+    const uint32_t xx_wgs = (n + kXxWaves * kXxPerWave - 1) / (kXxWaves * kXxPerWave);
     bool ok = true;
     auto h2d = [&](size_t o, const void *p, size_t bytes) {
         if (bytes) ok = ok && hipMemcpyAsync(ws + o, p, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
@@ -1214,6 +1337,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     h2d(o_blobs, blobs.data(), nb * sizeof(BlobDesc));
     h2d(o_blks, blks.data(), nk * sizeof(Blk));
     h2d(o_segs, segs.data(), ng * sizeof(Seg));
+    if (compress) h2d(o_xx, xx_ids.data(), nb * 4);
     if (encrypt) {
         h2d(o_rnd, random, nb * 56);
         h2d(o_key, key, 32);
@@ -1221,7 +1345,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     if (ok && n) {
         if (compress) {
             ok = hipEventRecord(C.fork, s) == hipSuccess && hipStreamWaitEvent(C.aux, C.fork, 0) == hipSuccess;
-            hipLaunchKernelGGL(k_xxh32, dim3((n + kXxWaves - 1) / kXxWaves), dim3(kXxWaves * 64), 0, C.aux, Bt);
+            hipLaunchKernelGGL(k_xxh32, dim3(xx_wgs), dim3(kXxWaves * 64), 0, C.aux, Bt);
             ok = ok && hipEventRecord(C.join, C.aux) == hipSuccess;
             if (ng) hipLaunchKernelGGL(k_lz4_seq, dim3(uint32_t((ng + kSeqWaves - 1) / kSeqWaves)), dim3(kSeqWaves * 64), 0, s, Bt);
             if (nk) hipLaunchKernelGGL(k_lz4_size, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
@@ -1229,7 +1353,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
         hipLaunchKernelGGL(k_enc_plan, dim3(1), dim3(kPlanThreads), 0, s, Bt);
         if (encrypt) hipLaunchKernelGGL(k_blob_keys, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
         if (compress) {
-            if (nk) hipLaunchKernelGGL(k_lz4_emit, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
+            if (nk) hipLaunchKernelGGL(k_lz4_emit, dim3(uint32_t(nk), kEmitSplit), dim3(kBlkThreads), 0, s, Bt);
             ok = ok && hipStreamWaitEvent(s, C.join, 0) == hipSuccess;  // the content checksums
             hipLaunchKernelGGL(k_frame_fin, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
         } else if (!encrypt) {

@@ -82,6 +82,39 @@ __device__ __forceinline__ uint64_t lds_gear(const char *tab, uint32_t addr)
     return *reinterpret_cast<const uint64_t *>(tab + addr);
 }
 
+// Address-space-typed views for code the compiler does not inline into its
+// kernel (next_node and what it calls): there a generic pointer becomes flat
+// loads, which count in both vmcnt and lgkmcnt, so each LDS wait also waits
+// for the global loads in flight (and LDS reads through flat are slower).
+typedef __attribute__((address_space(3))) const char lds_char;
+typedef __attribute__((address_space(1))) const uint64_t g_u64;
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+__device__ __forceinline__ uint64_t lds_gear(const lds_char *tab, uint32_t addr)
+{
+    return *reinterpret_cast<__attribute__((address_space(3))) const uint64_t *>(tab + addr);
+}
+
+template <typename T>
+__device__ __forceinline__ T *as_space(uint64_t addr)  // an address as a typed pointer
+{
+    return reinterpret_cast<T *>(uintptr_t(addr));
+}
+
+__device__ __forceinline__ const lds_char *as_lds(const char *p)  // LDS offset of a generic LDS pointer
+{
+    return as_space<const lds_char>(uint32_t(reinterpret_cast<uintptr_t>(p)));
+}
+
+// 16 bytes at a 16-B aligned global address (two 8-byte global loads).
+__device__ __forceinline__ uint4 gload16(uint64_t a)
+{
+    const g_u64 *q = as_space<const g_u64>(a);
+    const uint64_t x = q[0], y = q[1];
+    return make_uint4(uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32));
+}
+
 __device__ __forceinline__ uint32_t gear_addr(uint32_t laneoff, uint32_t word, int k)
 {
     // v_perm_b32: byte0 <- laneoff.byte0 (sel 4), byte1 <- word.byte(k), bytes 2,3 <- 0 (sel 0x0C)
@@ -117,8 +150,8 @@ __device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c)
 // Roll 16 bytes and return the min of the 16 keys (0 iff some position hit).
 // (Reducing the keys with v_min3 after the roll instead was 5 % slower on C3:
 // the keys stay live across the chain.)
-template <uint32_t ESH = kWEntShift>
-__device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, const char *tab,
+template <uint32_t ESH = kWEntShift, typename TP>
+__device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, TP tab,
                                                 uint32_t laneoff, uint32_t mlo, uint32_t mhi)
 {
     uint32_t acc = 0xFFFFFFFFu;
@@ -130,8 +163,8 @@ __device__ __forceinline__ uint32_t roll16_test(const uint4 &d, uint64_t &fp, co
     return acc;
 }
 
-template <uint32_t ESH = kWEntShift>
-__device__ __forceinline__ void roll16(const uint4 &d, uint64_t &fp, const char *tab,
+template <uint32_t ESH = kWEntShift, typename TP>
+__device__ __forceinline__ void roll16(const uint4 &d, uint64_t &fp, TP tab,
                                        uint32_t laneoff)
 {
 #pragma unroll
@@ -142,10 +175,10 @@ __device__ __forceinline__ void roll16(const uint4 &d, uint64_t &fp, const char 
 // General 16-byte group at absolute address a: positions < fz have fp = 0
 // (the reference resets fp at p+Min), positions in [ts, te) are tested.
 // Returns the first hit (absolute) or kNoHit; fp is advanced over the group.
-template <uint32_t ESH = kWEntShift>
+template <uint32_t ESH = kWEntShift, typename TP>
 __device__ __forceinline__ uint64_t group_first_hit(const uint4 &d, uint64_t &fp, uint64_t a,
                                                     uint64_t ts, uint64_t te, uint64_t fz,
-                                                    const char *tab, uint32_t laneoff,
+                                                    TP tab, uint32_t laneoff,
                                                     uint32_t mlo, uint32_t mhi)
 {
     uint64_t hit = kNoHit;
@@ -754,15 +787,15 @@ struct WalkCtx {
     uint64_t ub;       // absolute address of byte 0
     uint64_t len;
     uint32_t final_;
-    const uint64_t *runs;  // this buffer's index records (run q at runs[q])
+    const g_u64 *runs;     // this buffer's index records (run q at runs[q])
     uint64_t sl;           // run length (scan lane bytes)
     double inv_sl;
-    const char *tab;
+    const lds_char *tab;
     uint32_t laneoff;
     uint32_t lane;
     const uint64_t *gear;   // the 256-entry table in device memory
-    const uint64_t *runsL;  // this buffer's MaskL index records (null: no MaskL index)
-    const uint32_t *validL; // per scan task of the buffer: runsL holds its 64 records
+    const g_u64 *runsL;     // this buffer's MaskL index records (null: no MaskL index)
+    const g_u32 *validL;    // per scan task of the buffer: runsL holds its 64 records
 };
 
 // (A 32-copy table for long raw scans, filled on first use: C3 +2-4 %, C1 -4 %
@@ -773,7 +806,7 @@ struct WalkCtx {
 // after a 64-byte warm-up.  Positions are buffer-relative.  ESH selects the
 // table layout (8: 32 copies, v_perm addresses, conflict-free gathers).
 template <uint32_t ESH>
-__device__ uint64_t raw_scan(const WalkCtx &C, const char *tab, uint32_t laneoff, uint64_t lo, uint64_t hi,
+__device__ uint64_t raw_scan(const WalkCtx &C, const lds_char *tab, uint32_t laneoff, uint64_t lo, uint64_t hi,
                              uint64_t fz, uint32_t mlo, uint32_t mhi)
 {
     const uint64_t H = C.ub + hi, FZ = C.ub + fz;
@@ -791,7 +824,7 @@ __device__ uint64_t raw_scan(const WalkCtx &C, const char *tab, uint32_t laneoff
             const uint64_t hs = ts >= FZ + kWarm ? ts - kWarm : FZ;
             uint64_t fp = 0;
             for (uint64_t a = hs & ~15ull; a < te; a += 16) {
-                const uint4 d = *reinterpret_cast<const uint4 *>(a);
+                const uint4 d = gload16(a);
                 if (a >= FZ && a >= ts && a + 16 <= te) {
                     const uint64_t fp0 = fp;
                     if (roll16_test<ESH>(d, fp, tab, laneoff, mlo, mhi) == 0) {
@@ -980,7 +1013,7 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
     const bool rin = has_s && r0 + j <= rl;
     uint32_t byte = 0;
     uint64_t rec = 0;
-    if (tvalid) byte = reinterpret_cast<const uint8_t *>(C.ub)[tpos];
+    if (tvalid) byte = as_space<const g_u8>(C.ub)[tpos];
     if (rin) rec = C.runs[r0 + j];
     // ---- truncated window [fz, fz + W - 1)
     uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim, byte);
@@ -1076,7 +1109,7 @@ __device__ __forceinline__ uint64_t graph_succ(const WalkCtx &C, const DevParams
     const uint32_t sh = uint32_t(a & 3u);
     uint32_t dw[17];
 #pragma unroll
-    for (int k = 0; k < 17; ++k) dw[k] = *reinterpret_cast<const uint32_t *>(min<uint64_t>(a4 + 4u * uint64_t(k), last));
+    for (int k = 0; k < 17; ++k) dw[k] = *as_space<const g_u32>(min<uint64_t>(a4 + 4u * uint64_t(k), last));
     // ---- full-window MaskS candidates in [full0, s_end) from the records (while the bytes load)
     uint64_t full = kNoHit;  // kGHard: undecided by the records
     const uint64_t s_end = min(w.norm_end, w.lim);
@@ -1292,15 +1325,15 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.ub = reinterpret_cast<uint64_t>(D.data);
     C.len = D.len;
     C.final_ = B.final_;
-    C.runs = W.runs + 64ull * D.task_base;
+    C.runs = as_space<const g_u64>(reinterpret_cast<uintptr_t>(W.runs + 64ull * D.task_base));
     C.sl = B.scan_lane;
     C.inv_sl = 1.0 / double(B.scan_lane);
-    C.tab = tab;
+    C.tab = as_lds(tab);
     C.lane = threadIdx.x & 63u;
     C.laneoff = (C.lane & (kWCopies - 1u)) << 3;
     C.gear = W.gear;
-    C.runsL = B.maskl_index ? W.runsL + 64ull * D.task_base : nullptr;
-    C.validL = B.maskl_index ? W.validL + D.task_base : nullptr;
+    C.runsL = B.maskl_index ? as_space<const g_u64>(reinterpret_cast<uintptr_t>(W.runsL + 64ull * D.task_base)) : nullptr;
+    C.validL = B.maskl_index ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.validL + D.task_base)) : nullptr;
     return C;
 }
 
