@@ -242,12 +242,12 @@ def encode_leg(torch, batch, bufs, reps, baseline):
     plans = []
     for t, c in zip(bufs, cuts):
         c = c.cpu().numpy().astype(np.int64)
-        lens = c[:, 1].tolist()
-        cap = sum(encode.encode_bound(x) for x in lens)
-        plans.append((t, c[:, 0].tolist(), lens, torch.empty(max(cap, 1), dtype=torch.uint8, device=t.device)))
+        lens = c[:, 1].copy()
+        cap = sum(encode.encode_bound(int(x)) for x in lens)
+        plans.append((t, c[:, 0].copy(), lens, torch.empty(max(cap, 1), dtype=torch.uint8, device=t.device)))
     encoded = 0
     for t, offs, lens, out in plans:  # warm
-        encoded += encode.encode_device(t, offs, lens, out, key=key)[-1]
+        encoded += int(encode.encode_device(t, offs, lens, out, key=key)[-1])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):

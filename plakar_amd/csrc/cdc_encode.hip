@@ -452,7 +452,7 @@ __global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
 constexpr uint32_t kSeqWaves = 2;  // 24 KiB of LDS per wave: three workgroups per CU
 constexpr uint32_t kSkipShift = 6;  // LZ4's skip trigger
 
-struct SeqLds {
+struct alignas(16) SeqLds {
     uint32_t data[kSegLZ / 4 + 4];
     uint16_t tab[1u << kHashBits];
 };
@@ -478,18 +478,28 @@ __global__ __launch_bounds__(kSeqWaves * 64) void k_lz4_seq(const Batch B)
     const Seg S = B.segs[g];
     const uint8_t *src = B.base + S.src;
     const uint32_t n = S.len;
-    for (uint32_t i = lane; i < kSegLZ / 4 + 4; i += 64) {
-        const uint32_t p = 4 * i;
-        uint32_t v = 0;
-        if (p + 4 <= n) {
-            v = ld32u(src + p);
-        } else {
+    // the segment into LDS, 16 bytes per lane and load (unaligned global
+    // loads, all issued before the first store); a short segment's tail is
+    // zero-filled from byte loads
+    if (n == kSegLZ) {
+        uint4 v[kSegLZ / 1024];
 #pragma unroll
-            for (uint32_t b = 0; b < 4; ++b)
-                if (p + b < n) v |= uint32_t(src[p + b]) << (8 * b);
+        for (uint32_t j = 0; j < kSegLZ / 1024; ++j) __builtin_memcpy(&v[j], src + 1024 * j + 16 * lane, 16);
+#pragma unroll
+        for (uint32_t j = 0; j < kSegLZ / 1024; ++j) *reinterpret_cast<uint4 *>(&L.data[256 * j + 4 * lane]) = v[j];
+    } else for (uint32_t i = lane; i < kSegLZ / 16; i += 64) {
+        const uint32_t p = 16 * i;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (p + 16 <= n) {
+            __builtin_memcpy(&v, src + p, 16);
+        } else if (p < n) {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint32_t b = 0; p + b < n; ++b) w[b >> 2] |= uint32_t(src[p + b]) << (8 * (b & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        L.data[i] = v;
+        *reinterpret_cast<uint4 *>(&L.data[4 * i]) = v;
     }
+    if (lane < 4) L.data[kSegLZ / 4 + lane] = 0;
     for (uint32_t i = lane; i < (1u << kHashBits); i += 64) L.tab[i] = 0;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -995,15 +1005,16 @@ __global__ __launch_bounds__(64) void k_blob_keys(const Batch B)
     seal32(mk, r + 32, r, o + 12);
 }
 
-constexpr uint32_t kGcmWaves = 4;
+constexpr uint32_t kGcmWaves = 12;  // one workgroup per CU (LDS: the 64-KiB table), three waves per SIMD
 
-// LDS of a GCM workgroup.  The T-table in 32 copies, entry e of copy c at word
-// 32 e + c: lane l reads copy l & 31, so the 32 lanes of a ds_read_b32 group
-// always hit 32 distinct banks whatever the state bytes (the S-box of the
-// last round is byte 2 of the same entry).  rem8: the reduction of the 8 bits
-// a GHASH step shifts out.
+// LDS of a GCM workgroup.  The T-table in 64 copies, entry e of copy c at
+// byte 256 e + 4 c: lane l reads copy l, so its address is ONE v_perm of the
+// state word and the lane's offset (byte e in bits 8-15, 4 l in bits 0-7), and
+// the 32 lanes of each ds_read_b32 group hit 32 distinct banks whatever the
+// state bytes.  The S-box of the last round is byte 2 of the same entry.
+// rem8: the reduction of the 8 bits a GHASH step shifts out.
 struct GcmLds {
-    uint32_t te[256 * 32];
+    uint32_t te[256 * 64];
     uint64_t rem8[256];
     struct PerWave {
         uint32_t rk[60];
@@ -1013,30 +1024,42 @@ struct GcmLds {
     } w[kGcmWaves];
 };
 
-__device__ __forceinline__ void aes256_block_lds(const uint32_t *rk, const uint32_t *te, uint32_t c, uint32_t s[4])
+// Address of state byte k of word w in the 64-copy table.
+__device__ __forceinline__ uint32_t te_addr(uint32_t laneoff, uint32_t w, uint32_t k)
 {
-    auto T = [&](uint32_t x) { return te[(x << 5) | c]; };
+    return __builtin_amdgcn_perm(laneoff, w, 0x0C0C0004u | (k << 8));
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ void aes256_block_lds(const uint32_t *rk, const char *te, uint32_t laneoff, uint32_t s[4])
+{
+    auto T = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
     uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = T(s0 >> 24) ^ ror32(T((s1 >> 16) & 255), 8) ^ ror32(T((s2 >> 8) & 255), 16) ^
-                            ror32(T(s3 & 255), 24) ^ rk[4 * r];
-        const uint32_t t1 = T(s1 >> 24) ^ ror32(T((s2 >> 16) & 255), 8) ^ ror32(T((s3 >> 8) & 255), 16) ^
-                            ror32(T(s0 & 255), 24) ^ rk[4 * r + 1];
-        const uint32_t t2 = T(s2 >> 24) ^ ror32(T((s3 >> 16) & 255), 8) ^ ror32(T((s0 >> 8) & 255), 16) ^
-                            ror32(T(s1 & 255), 24) ^ rk[4 * r + 2];
-        const uint32_t t3 = T(s3 >> 24) ^ ror32(T((s0 >> 16) & 255), 8) ^ ror32(T((s1 >> 8) & 255), 16) ^
-                            ror32(T(s2 & 255), 24) ^ rk[4 * r + 3];
+        const uint32_t t0 = xor3(xor3(T(s0, 3), ror32(T(s1, 2), 8), ror32(T(s2, 1), 16)), ror32(T(s3, 0), 24), rk[4 * r]);
+        const uint32_t t1 = xor3(xor3(T(s1, 3), ror32(T(s2, 2), 8), ror32(T(s3, 1), 16)), ror32(T(s0, 0), 24), rk[4 * r + 1]);
+        const uint32_t t2 = xor3(xor3(T(s2, 3), ror32(T(s3, 2), 8), ror32(T(s0, 1), 16)), ror32(T(s1, 0), 24), rk[4 * r + 2]);
+        const uint32_t t3 = xor3(xor3(T(s3, 3), ror32(T(s0, 2), 8), ror32(T(s1, 1), 16)), ror32(T(s2, 0), 24), rk[4 * r + 3]);
         s0 = t0;
         s1 = t1;
         s2 = t2;
         s3 = t3;
     }
-    auto S = [&](uint32_t x) { return (T(x) >> 16) & 255u; };
-    s[0] = (S(s0 >> 24) << 24 | S((s1 >> 16) & 255) << 16 | S((s2 >> 8) & 255) << 8 | S(s3 & 255)) ^ rk[56];
-    s[1] = (S(s1 >> 24) << 24 | S((s2 >> 16) & 255) << 16 | S((s3 >> 8) & 255) << 8 | S(s0 & 255)) ^ rk[57];
-    s[2] = (S(s2 >> 24) << 24 | S((s3 >> 16) & 255) << 16 | S((s0 >> 8) & 255) << 8 | S(s1 & 255)) ^ rk[58];
-    s[3] = (S(s3 >> 24) << 24 | S((s0 >> 16) & 255) << 16 | S((s1 >> 8) & 255) << 8 | S(s2 & 255)) ^ rk[59];
+    // last round: S-box bytes (byte 2 of the T entries) gathered by v_perm
+    auto S4 = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        const uint32_t hi = __builtin_amdgcn_perm(T(a, 3), T(b, 2), 0x0602FFFFu);  // [Sa, Sb, -, -]
+        const uint32_t lo = __builtin_amdgcn_perm(T(c, 1), T(d, 0), 0xFFFF0602u);  // [-, -, Sc, Sd]
+        return (hi & 0xFFFF0000u) | (lo & 0xFFFFu);
+    };
+    s[0] = S4(s0, s1, s2, s3) ^ rk[56];
+    s[1] = S4(s1, s2, s3, s0) ^ rk[57];
+    s[2] = S4(s2, s3, s0, s1) ^ rk[58];
+    s[3] = S4(s3, s0, s1, s2) ^ rk[59];
 }
 
 // x * V with V's 8-bit table (byte by byte from the last).
@@ -1061,14 +1084,15 @@ __device__ __forceinline__ uint32_t be32(uint32_t x) { return __builtin_bswap32(
 __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
 {
     __shared__ GcmLds L;
-    for (uint32_t i = threadIdx.x; i < 256 * 32; i += blockDim.x) L.te[i] = g_te0[i >> 5];
+    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) L.te[i] = g_te0[i >> 6];
     for (uint32_t r = threadIdx.x; r < 256; r += blockDim.x) {
         uint64_t x = 0;
         for (uint32_t b = 0; b < 8; ++b)
             if (r & (1u << b)) x ^= uint64_t(0xE100u >> (7 - b));
         L.rem8[r] = x << 48;
     }
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, cpy = lane & 31u;
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, laneoff = lane << 2;
+    const char *te = reinterpret_cast<const char *>(L.te);
     const uint32_t pc = blockIdx.x * kGcmWaves + wv;
     const uint32_t total = B.piece_base[B.nblobs];
     const bool active = pc < total && !B.status[0];
@@ -1117,7 +1141,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         uint4 cw = make_uint4(0, 0, 0, 0);
         if (i < nb) {
             uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
-            aes256_block_lds(rk, L.te, cpy, c);
+            aes256_block_lds(rk, te, laneoff, c);
             const uint32_t bytes = min(16u, m - 16 * i);
             uint32_t pw[4];
             if (pt_al && bytes == 16) {
@@ -1169,7 +1193,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     if (lane == 0) {
         G128 S = gmul4(gx(Z, G128{0, uint64_t(m) * 8}), L.w[wv].th);
         uint32_t t[4] = {j0[0], j0[1], j0[2], 1};
-        aes256_block_lds(rk, L.te, cpy, t);
+        aes256_block_lds(rk, te, laneoff, t);
         const uint64_t hi = S.hi ^ (uint64_t(t[0]) << 32 | t[1]), lo = S.lo ^ (uint64_t(t[2]) << 32 | t[3]);
         uint8_t *tag = ct + m;
         for (int q = 0; q < 8; ++q) {

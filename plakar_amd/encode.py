@@ -20,14 +20,18 @@ def encode_bound(n, compress=True, encrypt=True):
 
 def encode_device(base, offsets, lens, out, key=None, compress=True, random=None, device=0, stream=None):
     """Encode blobs that live in the device tensor `base` (uint8) at the given
-    byte offsets/lengths into the device tensor `out`; returns the n + 1
-    output offsets."""
+    byte offsets/lengths (sequences or numpy arrays) into the device tensor
+    `out`; returns the n + 1 output offsets (int64 numpy array)."""
     import torch
     ensure_init()
     n = len(lens)
-    offs = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in offsets])
-    lns = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
-    oo = (ctypes.c_uint64 * (n + 1))()
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    offs_a = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64).reshape(-1))
+    lens_a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64).reshape(-1))
+    if offs_a.size != n:
+        raise ValueError("offsets and lens differ in length")
+    oo_a = np.zeros(n + 1, dtype=np.uint64)
+    offs, lns, oo = (a.ctypes.data_as(u64p) if a.size else (ctypes.c_uint64 * 1)() for a in (offs_a, lens_a, oo_a))
     if key is not None:
         key = bytes(key)
         if len(key) != 32:
@@ -40,7 +44,7 @@ def encode_device(base, offsets, lens, out, key=None, compress=True, random=None
     check(lib().cdc_encode_device(int(device), ctypes.c_void_p(base.data_ptr()), offs, lns, n, int(bool(compress)),
                                   key, bytes(random) if key is not None else None, ctypes.c_void_p(out.data_ptr()),
                                   out.numel(), oo, ctypes.c_void_p(st.cuda_stream)), "cdc_encode_device")
-    return [int(oo[i]) for i in range(n + 1)]
+    return oo_a.astype(np.int64)
 
 
 def encode_blobs(blobs, key=None, compress=True, random=None, device=0):
@@ -58,7 +62,7 @@ def encode_blobs(blobs, key=None, compress=True, random=None, device=0):
     cap = sum(encode_bound(n, compress, key is not None) for n in lens)
     out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
     oo = encode_device(base, offs[:-1], lens, out, key=key, compress=compress, random=random, device=device)
-    host = out[:oo[-1]].cpu().numpy()
+    host = out[:int(oo[-1])].cpu().numpy()
     return [host[oo[i]:oo[i + 1]].tobytes() for i in range(len(lens))]
 
 

@@ -147,7 +147,7 @@ def test_encode_device_resident_batch():
     for i, (o, n) in enumerate(cuts):
         enc = host[oo[i]:oo[i + 1]].tobytes()
         assert ref.decode(enc, key=KEY) == data[o:o + n].tobytes()
-    small = torch.empty(oo[-1] - 1, dtype=torch.uint8, device="cuda")
+    small = torch.empty(int(oo[-1]) - 1, dtype=torch.uint8, device="cuda")
     with pytest.raises(_lib.CdcError):
         encode.encode_device(t, offs, lens, small, key=KEY)
 

@@ -35,7 +35,7 @@ def main():
         b.launch()
         (cuts,), _ = b.results()
         c = cuts.cpu().numpy().astype(np.int64)
-        offs, lens = c[:, 0].tolist(), c[:, 1].tolist()
+        offs, lens = c[:, 0].copy(), c[:, 1].copy()
         for label, k, comp in (("lz4+gcm", key, True), ("lz4", None, True), ("gcm", key, False)):
             cap = sum(encode.encode_bound(x, comp, k is not None) for x in lens)
             out = torch.empty(cap, dtype=torch.uint8, device="cuda")
