@@ -21,8 +21,10 @@
 //                 GCM pieces and output offsets of every blob (scans)
 //   k_lz4_emit    a workgroup per block (16 per stored block): its bytes
 //   k_frame_fin   one wave per blob: frame header, end mark, checksum
-//   k_blob_keys   one lane per blob: the subkey's round keys, H and its
-//                 powers H^1..H^64, and the sealed subkey (header)
+//   k_blob_keys   one thread per blob: the subkey's round keys, H and its
+//                 4-bit table, and the sealed subkey (header)
+//   k_blob_pows   one wave per blob: H^1..H^64 (a doubling ladder over the
+//                 lanes) and the 8-bit table of H^64
 //   k_gcm         one wave per 64-KiB piece: AES-256-CTR (T-table in LDS,
 //                 32 bank-conflict-free copies) and GHASH (lane l hashes
 //                 blocks l, l+64, ... by Horner in H^64 with an 8-bit table,
@@ -230,20 +232,6 @@ struct BlobKey {
     G128 hpow[64];    // H^1 .. H^64
     G128 t64[256];    // 8-bit table of H^64 (the lanes' Horner steps)
 };
-
-// 8-bit table: T[i] = i * V for the byte i read MSB-first (T[128] = V).
-__device__ void gtable8(G128 v, G128 *t)
-{
-    auto half = [](G128 x) {
-        const uint64_t r = (x.lo & 1) ? 0xE100000000000000ull : 0;
-        return G128{(x.hi >> 1) ^ r, (x.lo >> 1) | (x.hi << 63)};
-    };
-    t[0] = {0, 0};
-    t[128] = v;
-    for (int i = 64; i; i >>= 1) t[i] = half(t[2 * i]);
-    for (int i = 2; i < 256; i <<= 1)
-        for (int j = 1; j < i; ++j) t[i + j] = gx(t[i], t[j]);
-}
 
 struct Seg {             // a 16-KiB LZ4 search segment
     uint64_t src;        // byte offset in the input base
@@ -935,74 +923,143 @@ __device__ __forceinline__ void gcm_block_words(const uint8_t *p, uint32_t w[4])
         w[i] = uint32_t(p[4 * i]) << 24 | uint32_t(p[4 * i + 1]) << 16 | uint32_t(p[4 * i + 2]) << 8 | p[4 * i + 3];
 }
 
-// One lane: Seal(key, nonce, pt[0..32)) -> ct (32) || tag (16), for the
-// subkey header (two blocks, no AAD).
-__device__ void seal32(const uint32_t rk[60], const uint8_t nonce[12], const uint8_t pt[32], uint8_t *out)
+// Key setup, in two kernels.  k_blob_keys: one thread per blob (the AES
+// tables and the repository key's schedule, H and 4-bit table in LDS, shared
+// by the workgroup): the subkey's round keys, H = AES_K(0) and its 4-bit
+// table, and the stream header (subkey nonce || Seal(repository key, subkey
+// nonce, subkey)).  k_blob_pows: one wave per blob: H^1..H^64 by a doubling
+// ladder (round k: lanes [2^k, 2^(k+1)) multiply H^(lane + 1 - 2^k) by H^(2^k)
+// with its 4-bit table, built by 16 lanes), then four entries per lane of the
+// 8-bit table of H^64 from its eight halvings.
+constexpr uint32_t kKeyThreads = 256;
+constexpr uint32_t kPowWaves = 4;
+
+__device__ __forceinline__ G128 ghalf(G128 x)  // x times the field's x (one right shift with reduction)
 {
-    uint32_t z[4] = {0, 0, 0, 0};
-    aes256_block(rk, g_te0, g_sbox, z);
-    G128 th[16];
-    gtable(g_from_words(z), th);
-    uint32_t j0[4];
-    j0[0] = uint32_t(nonce[0]) << 24 | uint32_t(nonce[1]) << 16 | uint32_t(nonce[2]) << 8 | nonce[3];
-    j0[1] = uint32_t(nonce[4]) << 24 | uint32_t(nonce[5]) << 16 | uint32_t(nonce[6]) << 8 | nonce[7];
-    j0[2] = uint32_t(nonce[8]) << 24 | uint32_t(nonce[9]) << 16 | uint32_t(nonce[10]) << 8 | nonce[11];
-    j0[3] = 1;
-    G128 S = {0, 0};
-    for (uint32_t i = 0; i < 2; ++i) {
-        uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
-        aes256_block(rk, g_te0, g_sbox, c);
-        uint32_t p[4];
-        gcm_block_words(pt + 16 * i, p);
-        for (int k = 0; k < 4; ++k) {
-            c[k] ^= p[k];
-            out[16 * i + 4 * k] = uint8_t(c[k] >> 24);
-            out[16 * i + 4 * k + 1] = uint8_t(c[k] >> 16);
-            out[16 * i + 4 * k + 2] = uint8_t(c[k] >> 8);
-            out[16 * i + 4 * k + 3] = uint8_t(c[k]);
-        }
-        S = gmul4(gx(S, g_from_words(c)), th);
-    }
-    S = gmul4(gx(S, G128{0, 256}), th);  // len(A) = 0, len(C) = 256 bits
-    uint32_t t[4] = {j0[0], j0[1], j0[2], j0[3]};
-    aes256_block(rk, g_te0, g_sbox, t);
-    const uint64_t hi = S.hi ^ (uint64_t(t[0]) << 32 | t[1]), lo = S.lo ^ (uint64_t(t[2]) << 32 | t[3]);
-    for (int k = 0; k < 8; ++k) {
-        out[32 + k] = uint8_t(hi >> (56 - 8 * k));
-        out[40 + k] = uint8_t(lo >> (56 - 8 * k));
-    }
+    const uint64_t r = (x.lo & 1) ? 0xE100000000000000ull : 0;
+    return G128{(x.hi >> 1) ^ r, (x.lo >> 1) | (x.hi << 63)};
 }
 
-__global__ __launch_bounds__(64) void k_blob_keys(const Batch B)
+__global__ __launch_bounds__(kKeyThreads) void k_blob_keys(const Batch B)
 {
-    const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+    __shared__ uint32_t s_te[256];
+    __shared__ uint8_t s_sb[256];
+    __shared__ uint32_t s_mrk[60];
+    __shared__ G128 s_mth[16];
+    const uint32_t t = threadIdx.x;
+    s_te[t] = g_te0[t];
+    s_sb[t] = g_sbox[t];
+    __syncthreads();
+    if (t == 0) {  // the repository key: schedule, H and its table
+        uint8_t key[32];
+        for (int i = 0; i < 32; ++i) key[i] = B.key[i];
+        uint32_t mk[60];
+        aes256_expand(key, mk, s_sb);
+        for (int i = 0; i < 60; ++i) s_mrk[i] = mk[i];
+        uint32_t z[4] = {0, 0, 0, 0};
+        aes256_block(mk, s_te, s_sb, z);
+        G128 th[16];
+        gtable(g_from_words(z), th);
+        for (int i = 0; i < 16; ++i) s_mth[i] = th[i];
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x * kKeyThreads + t;
     if (b >= B.nblobs || B.status[0]) return;
     const uint8_t *r = B.rnd + 56ull * b;  // subkey 32, subkey nonce 12, data nonce 12
     BlobKey &K = B.keys[b];
-    uint32_t rk[60];
-    aes256_expand(r, rk, g_sbox);
-    for (int i = 0; i < 60; ++i) K.rk[i] = rk[i];
-    uint32_t z[4] = {0, 0, 0, 0};
-    aes256_block(rk, g_te0, g_sbox, z);
-    const G128 H = g_from_words(z);
-    G128 th[16];
-    gtable(H, th);
-    for (int i = 0; i < 16; ++i) K.th[i] = th[i];
-    G128 p = H;
-    K.hpow[0] = H;
-    for (int e = 1; e < 64; ++e) {
-        p = gmul4(p, th);
-        K.hpow[e] = p;
+    {
+        uint32_t rk[60];
+        aes256_expand(r, rk, s_sb);
+        for (int i = 0; i < 60; ++i) K.rk[i] = rk[i];
+        uint32_t z[4] = {0, 0, 0, 0};
+        aes256_block(rk, s_te, s_sb, z);
+        const G128 H = g_from_words(z);
+        K.hpow[0] = H;
+        G128 th[16];
+        gtable(H, th);
+        for (int i = 0; i < 16; ++i) K.th[i] = th[i];
     }
-    gtable8(p, K.t64);
     // header: subkey nonce || Seal(repository key, subkey nonce, subkey)
     uint8_t *o = B.out + B.out_off[b];
     for (int i = 0; i < 12; ++i) o[i] = r[32 + i];
-    uint32_t mk[60];
-    uint8_t key[32];
-    for (int i = 0; i < 32; ++i) key[i] = B.key[i];
-    aes256_expand(key, mk, g_sbox);
-    seal32(mk, r + 32, r, o + 12);
+    const uint8_t *nonce = r + 32;
+    uint32_t j0[3];
+    j0[0] = uint32_t(nonce[0]) << 24 | uint32_t(nonce[1]) << 16 | uint32_t(nonce[2]) << 8 | nonce[3];
+    j0[1] = uint32_t(nonce[4]) << 24 | uint32_t(nonce[5]) << 16 | uint32_t(nonce[6]) << 8 | nonce[7];
+    j0[2] = uint32_t(nonce[8]) << 24 | uint32_t(nonce[9]) << 16 | uint32_t(nonce[10]) << 8 | nonce[11];
+    G128 S = {0, 0};
+    for (uint32_t i = 0; i < 2; ++i) {
+        uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
+        aes256_block(s_mrk, s_te, s_sb, c);
+        uint32_t p[4];
+        gcm_block_words(r + 16 * i, p);
+        for (int k = 0; k < 4; ++k) {
+            c[k] ^= p[k];
+            o[12 + 16 * i + 4 * k] = uint8_t(c[k] >> 24);
+            o[12 + 16 * i + 4 * k + 1] = uint8_t(c[k] >> 16);
+            o[12 + 16 * i + 4 * k + 2] = uint8_t(c[k] >> 8);
+            o[12 + 16 * i + 4 * k + 3] = uint8_t(c[k]);
+        }
+        S = gmul4(gx(S, g_from_words(c)), s_mth);
+    }
+    S = gmul4(gx(S, G128{0, 256}), s_mth);  // len(A) = 0, len(C) = 256 bits
+    uint32_t tg[4] = {j0[0], j0[1], j0[2], 1};
+    aes256_block(s_mrk, s_te, s_sb, tg);
+    const uint64_t hi = S.hi ^ (uint64_t(tg[0]) << 32 | tg[1]), lo = S.lo ^ (uint64_t(tg[2]) << 32 | tg[3]);
+    for (int k = 0; k < 8; ++k) {
+        o[44 + k] = uint8_t(hi >> (56 - 8 * k));
+        o[52 + k] = uint8_t(lo >> (56 - 8 * k));
+    }
+}
+
+__global__ __launch_bounds__(kPowWaves * 64) void k_blob_pows(const Batch B)
+{
+    struct PowLds {
+        G128 pw[64];
+        G128 tab[16];
+    };
+    __shared__ PowLds S[kPowWaves];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t b = blockIdx.x * kPowWaves + wv;
+    if (b >= B.nblobs || B.status[0]) return;
+    PowLds &L = S[wv];
+    BlobKey &K = B.keys[b];
+    if (lane == 0) L.pw[0] = K.hpow[0];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t m = 1; m < 64; m <<= 1) {
+        if (lane < 16) {  // 4-bit table of X = H^m: entry i = XOR of X * x^(3 - j) over the bits j of i
+            G128 v = L.pw[m - 1], e = {0, 0};
+#pragma unroll
+            for (int j = 3; j >= 0; --j) {
+                if ((lane >> j) & 1) e = gx(e, v);
+                v = ghalf(v);
+            }
+            L.tab[lane] = e;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        if (lane >= m && lane < 2 * m) L.pw[lane] = gmul4(L.pw[lane - m], L.tab);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+    }
+    K.hpow[lane] = L.pw[lane];
+    // 8-bit table of V = H^64: T[i] = XOR of v_j over the bits j of i, v_7 = V,
+    // v_(j-1) = v_j * x (a halving)
+    G128 v[8];
+    v[7] = L.pw[63];
+#pragma unroll
+    for (int j = 7; j > 0; --j) v[j - 1] = ghalf(v[j]);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * lane + q;
+        G128 e = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if ((i >> j) & 1) e = gx(e, v[j]);
+        K.t64[i] = e;
+    }
 }
 
 constexpr uint32_t kGcmWaves = 12;  // one workgroup per CU (LDS: the 64-KiB table), three waves per SIMD
@@ -1020,7 +1077,7 @@ struct GcmLds {
         uint32_t rk[60];
         G128 th[16];
         G128 t64[256];
-        uint4 stage[64];
+        uint4 stage[128];
     } w[kGcmWaves];
 };
 
@@ -1035,20 +1092,28 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-__device__ __forceinline__ void aes256_block_lds(const uint32_t *rk, const char *te, uint32_t laneoff, uint32_t s[4])
+// N independent blocks at once (their table lookups interleave: more LDS
+// reads in flight per wave).
+template <int N>
+__device__ __forceinline__ void aes256_blocks_lds(const uint32_t *rk, const char *te, uint32_t laneoff, uint32_t (&st)[N][4])
 {
     auto T = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
-    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+    uint32_t s[N][4];
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+        for (int q = 0; q < 4; ++q) s[n][q] = st[n][q] ^ rk[q];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = xor3(xor3(T(s0, 3), ror32(T(s1, 2), 8), ror32(T(s2, 1), 16)), ror32(T(s3, 0), 24), rk[4 * r]);
-        const uint32_t t1 = xor3(xor3(T(s1, 3), ror32(T(s2, 2), 8), ror32(T(s3, 1), 16)), ror32(T(s0, 0), 24), rk[4 * r + 1]);
-        const uint32_t t2 = xor3(xor3(T(s2, 3), ror32(T(s3, 2), 8), ror32(T(s0, 1), 16)), ror32(T(s1, 0), 24), rk[4 * r + 2]);
-        const uint32_t t3 = xor3(xor3(T(s3, 3), ror32(T(s0, 2), 8), ror32(T(s1, 1), 16)), ror32(T(s2, 0), 24), rk[4 * r + 3]);
-        s0 = t0;
-        s1 = t1;
-        s2 = t2;
-        s3 = t3;
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            uint32_t t[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                t[q] = xor3(xor3(T(s[n][q], 3), ror32(T(s[n][(q + 1) & 3], 2), 8), ror32(T(s[n][(q + 2) & 3], 1), 16)),
+                            ror32(T(s[n][(q + 3) & 3], 0), 24), rk[4 * r + q]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s[n][q] = t[q];
+        }
     }
     // last round: S-box bytes (byte 2 of the T entries) gathered by v_perm
     auto S4 = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -1056,10 +1121,11 @@ __device__ __forceinline__ void aes256_block_lds(const uint32_t *rk, const char 
         const uint32_t lo = __builtin_amdgcn_perm(T(c, 1), T(d, 0), 0xFFFF0602u);  // [-, -, Sc, Sd]
         return (hi & 0xFFFF0000u) | (lo & 0xFFFFu);
     };
-    s[0] = S4(s0, s1, s2, s3) ^ rk[56];
-    s[1] = S4(s1, s2, s3, s0) ^ rk[57];
-    s[2] = S4(s2, s3, s0, s1) ^ rk[58];
-    s[3] = S4(s3, s0, s1, s2) ^ rk[59];
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            st[n][q] = S4(s[n][q], s[n][(q + 1) & 3], s[n][(q + 2) & 3], s[n][(q + 3) & 3]) ^ rk[56 + q];
 }
 
 // x * V with V's 8-bit table (byte by byte from the last).
@@ -1132,51 +1198,63 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint32_t *rk = L.w[wv].rk;
     const G128 *t64 = L.w[wv].t64;
     uint8_t *stage = reinterpret_cast<uint8_t *>(L.w[wv].stage);
-    // row j: blocks 64 j + lane (1 KiB of the piece); lane: Horner in H^64 over its blocks
+    // row j: blocks 64 j + lane (1 KiB of the piece), two rows per step (their
+    // AES interleaved); lane: Horner in H^64 over its blocks, in order
     G128 Z = {0, 0};
     uint32_t cnt = 0;
     const uint32_t rows = (nb + 63) / 64;
-    for (uint32_t j = 0; j < rows; ++j) {
-        const uint32_t i = 64 * j + lane;
-        uint4 cw = make_uint4(0, 0, 0, 0);
-        if (i < nb) {
-            uint32_t c[4] = {j0[0], j0[1], j0[2], 2 + i};
-            aes256_block_lds(rk, te, laneoff, c);
-            const uint32_t bytes = min(16u, m - 16 * i);
-            uint32_t pw[4];
-            if (pt_al && bytes == 16) {
-                const gu32 *q = reinterpret_cast<const gu32 *>(pt + 16 * i);
-                for (int k = 0; k < 4; ++k) pw[k] = be32(q[k]);
-            } else if (bytes == 16) {  // aligned dwords + v_alignbit (the last one holds needed bytes)
-                const gu32 *aw = reinterpret_cast<const gu32 *>(reinterpret_cast<uintptr_t>(pt + 16 * i) & ~uintptr_t(3));
-                const uint32_t sh = pt_sh * 8u;
-                uint32_t x[5];
-                for (int q = 0; q < 4; ++q) x[q] = aw[q];
-                x[4] = sh ? aw[4] : 0u;
-                for (int q = 0; q < 4; ++q) pw[q] = be32(sh ? __builtin_amdgcn_alignbit(x[q + 1], x[q], sh) : x[q]);
-            } else {
-                uint8_t blk[16];
-                for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
-                gcm_block_words(blk, pw);
-            }
-            uint32_t w[4];
-            for (int q = 0; q < 4; ++q) w[q] = c[q] ^ pw[q];
-            if (bytes < 16) {  // the keystream past the piece's end is not ciphertext (nor hashed)
-                for (int q = 0; q < 4; ++q) {
-                    const int keep = int(bytes) - 4 * q;
-                    w[q] = keep >= 4 ? w[q] : keep <= 0 ? 0u : (w[q] & ~(0xFFFFFFFFu >> (8 * keep)));
-                }
-            }
-            cw = make_uint4(be32(w[0]), be32(w[1]), be32(w[2]), be32(w[3]));
-            Z = gx(gmul8(Z, t64, L.rem8), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
-            ++cnt;
-        }
-        // the row's ciphertext through LDS: 16 coalesced byte stores of 64 bytes
-        L.w[wv].stage[lane] = cw;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t row_bytes = min(1024u, m - 1024 * j);
+    for (uint32_t j = 0; j < rows; j += 2) {
+        uint32_t c[2][4];
 #pragma unroll
-        for (uint32_t q = 0; q < 16; ++q) {
+        for (int u = 0; u < 2; ++u) {
+            c[u][0] = j0[0];
+            c[u][1] = j0[1];
+            c[u][2] = j0[2];
+            c[u][3] = 2 + 64 * (j + u) + lane;
+        }
+        aes256_blocks_lds<2>(rk, te, laneoff, c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t i = 64 * (j + u) + lane;
+            uint4 cw = make_uint4(0, 0, 0, 0);
+            if (i < nb) {
+                const uint32_t bytes = min(16u, m - 16 * i);
+                uint32_t pw[4];
+                if (pt_al && bytes == 16) {
+                    const gu32 *q = reinterpret_cast<const gu32 *>(pt + 16 * i);
+                    for (int k = 0; k < 4; ++k) pw[k] = be32(q[k]);
+                } else if (bytes == 16) {  // aligned dwords + v_alignbit (the last one holds needed bytes)
+                    const gu32 *aw =
+                        reinterpret_cast<const gu32 *>(reinterpret_cast<uintptr_t>(pt + 16 * i) & ~uintptr_t(3));
+                    const uint32_t sh = pt_sh * 8u;
+                    uint32_t x[5];
+                    for (int q = 0; q < 4; ++q) x[q] = aw[q];
+                    x[4] = sh ? aw[4] : 0u;
+                    for (int q = 0; q < 4; ++q) pw[q] = be32(sh ? __builtin_amdgcn_alignbit(x[q + 1], x[q], sh) : x[q]);
+                } else {
+                    uint8_t blk[16];
+                    for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
+                    gcm_block_words(blk, pw);
+                }
+                uint32_t w[4];
+                for (int q = 0; q < 4; ++q) w[q] = c[u][q] ^ pw[q];
+                if (bytes < 16) {  // the keystream past the piece's end is not ciphertext (nor hashed)
+                    for (int q = 0; q < 4; ++q) {
+                        const int keep = int(bytes) - 4 * q;
+                        w[q] = keep >= 4 ? w[q] : keep <= 0 ? 0u : (w[q] & ~(0xFFFFFFFFu >> (8 * keep)));
+                    }
+                }
+                cw = make_uint4(be32(w[0]), be32(w[1]), be32(w[2]), be32(w[3]));
+                Z = gx(gmul8(Z, t64, L.rem8), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
+                ++cnt;
+            }
+            L.w[wv].stage[64 * u + lane] = cw;
+        }
+        // the rows' ciphertext through LDS: 32 coalesced byte stores of 64 bytes
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t row_bytes = min(2048u, m - 1024 * j);
+#pragma unroll
+        for (uint32_t q = 0; q < 32; ++q) {
             const uint32_t x = 64 * q + lane;
             if (x < row_bytes) ct[1024 * j + x] = stage[x];
         }
@@ -1192,9 +1270,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     }
     if (lane == 0) {
         G128 S = gmul4(gx(Z, G128{0, uint64_t(m) * 8}), L.w[wv].th);
-        uint32_t t[4] = {j0[0], j0[1], j0[2], 1};
-        aes256_block_lds(rk, te, laneoff, t);
-        const uint64_t hi = S.hi ^ (uint64_t(t[0]) << 32 | t[1]), lo = S.lo ^ (uint64_t(t[2]) << 32 | t[3]);
+        uint32_t t[1][4] = {{j0[0], j0[1], j0[2], 1}};
+        aes256_blocks_lds<1>(rk, te, laneoff, t);
+        const uint64_t hi = S.hi ^ (uint64_t(t[0][0]) << 32 | t[0][1]), lo = S.lo ^ (uint64_t(t[0][2]) << 32 | t[0][3]);
         uint8_t *tag = ct + m;
         for (int q = 0; q < 8; ++q) {
             tag[q] = uint8_t(hi >> (56 - 8 * q));
@@ -1375,7 +1453,10 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
             if (nk) hipLaunchKernelGGL(k_lz4_size, dim3(uint32_t(nk)), dim3(kBlkThreads), 0, s, Bt);
         }
         hipLaunchKernelGGL(k_enc_plan, dim3(1), dim3(kPlanThreads), 0, s, Bt);
-        if (encrypt) hipLaunchKernelGGL(k_blob_keys, dim3((n + 63) / 64), dim3(64), 0, s, Bt);
+        if (encrypt) {
+            hipLaunchKernelGGL(k_blob_keys, dim3((n + kKeyThreads - 1) / kKeyThreads), dim3(kKeyThreads), 0, s, Bt);
+            hipLaunchKernelGGL(k_blob_pows, dim3((n + kPowWaves - 1) / kPowWaves), dim3(kPowWaves * 64), 0, s, Bt);
+        }
         if (compress) {
             if (nk) hipLaunchKernelGGL(k_lz4_emit, dim3(uint32_t(nk), kEmitSplit), dim3(kBlkThreads), 0, s, Bt);
             ok = ok && hipStreamWaitEvent(s, C.join, 0) == hipSuccess;  // the content checksums
