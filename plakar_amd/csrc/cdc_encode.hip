@@ -47,10 +47,10 @@
 
 namespace enc {
 
-constexpr uint32_t kSegLZ = 16384;            // LZ4 match-search segment
+constexpr uint32_t kSegLZ = 8192;             // LZ4 match-search segment
 constexpr uint64_t kBlockLZ = 4ull << 20;     // LZ4 block (pierrec Block4Mb)
 constexpr uint32_t kPiece = 65536;            // EncryptStream chunkSize
-constexpr uint32_t kHashBits = 12;
+constexpr uint32_t kHashBits = 11;
 constexpr uint32_t kRecCap = kSegLZ / 4 + 2;  // records per segment (a match per 4 bytes at most)
 
 // ---------------------------------------------------------------------------
@@ -270,6 +270,7 @@ struct Batch {
     uint2 *recs;              // kRecCap per segment
     uint32_t *nrec;           // per segment
     uint32_t *trail;          // per segment: literals after its last match (from its start when none)
+    uint32_t *seg_out;        // per segment: bytes of its sequences in the block (k_lz4_size)
     uint32_t *blk_size;       // per block: encoded size, bit 31 = stored raw
     uint64_t *blk_foff;       // per block: offset of its header in the frame
     uint32_t *xxh;            // per blob
@@ -576,7 +577,9 @@ constexpr uint32_t kMaxSegsPerBlk = uint32_t(kBlockLZ / kSegLZ);
 struct BlkLds {
     uint32_t rbase[kMaxSegsPerBlk + 1];  // first record index (block-relative) of each segment
     uint32_t prev_end[kMaxSegsPerBlk];   // block-relative end of the last match before each segment
-    uint32_t tile_off[kBlkThreads];
+    uint32_t obase[kMaxSegsPerBlk + 1];  // output offset of each segment's first sequence (emit)
+    uint32_t acc[kMaxSegsPerBlk];        // per-segment sequence bytes (size)
+    uint32_t wsum[3][kBlkThreads / 64];
     uint64_t total;
 };
 
@@ -604,23 +607,72 @@ __device__ __forceinline__ uint32_t seq_size(uint32_t lit_len, uint32_t mlen)
     return 1 + ext_len(lit_len) + lit_len + 2 + ext_len(mlen - 4);
 }
 
-// Shared prologue: per-segment record bases and the match end before each segment.
-__device__ void blk_prologue(const Batch &B, const Blk &K, BlkLds &L)
+// Shared prologue: per-segment record bases, the match end before each
+// segment and (emit) each segment's output offset: a thread per kPerThr
+// consecutive segments, exclusive sum / max scans over the workgroup.
+constexpr uint32_t kPerThr = (kMaxSegsPerBlk + kBlkThreads - 1) / kBlkThreads;
+
+__device__ void blk_prologue(const Batch &B, const Blk &K, BlkLds &L, bool with_out)
 {
-    if (threadIdx.x == 0) {
-        uint32_t base = 0, end = 0;
-        for (uint32_t s = 0; s < K.nseg; ++s) {
-            L.rbase[s] = base;
-            L.prev_end[s] = end;
-            const uint32_t nr = B.nrec[K.seg0 + s];
-            if (nr) {
-                const uint2 y = B.recs[uint64_t(K.seg0 + s) * kRecCap + nr - 1];
-                end = s * kSegLZ + (y.x & 0xFFFFu) + y.y;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    uint32_t nr[kPerThr], en[kPerThr], ob[kPerThr];
+    uint32_t c = 0, m = 0, o = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPerThr; ++k) {
+        const uint32_t sg = t * kPerThr + k;
+        nr[k] = en[k] = ob[k] = 0;
+        if (sg < K.nseg) {
+            nr[k] = B.nrec[K.seg0 + sg];
+            if (nr[k]) {
+                const uint2 y = B.recs[uint64_t(K.seg0 + sg) * kRecCap + nr[k] - 1];
+                en[k] = sg * kSegLZ + (y.x & 0xFFFFu) + y.y;
             }
-            base += nr;
+            if (with_out) ob[k] = B.seg_out[K.seg0 + sg];
         }
-        L.rbase[K.nseg] = base;
-        L.total = end;  // the last match's end: the final literal run starts here
+        c += nr[k];
+        m = max(m, en[k]);
+        o += ob[k];
+    }
+    // inclusive scans over the wave, then over the waves
+    uint32_t ic = c, im = m, io = o;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t yc = __shfl_up(ic, d), ym = __shfl_up(im, d), yo = __shfl_up(io, d);
+        if (lane >= d) {
+            ic += yc;
+            im = max(im, ym);
+            io += yo;
+        }
+    }
+    if (lane == 63) {
+        L.wsum[0][wv] = ic;
+        L.wsum[1][wv] = im;
+        L.wsum[2][wv] = io;
+    }
+    __syncthreads();
+    uint32_t bc = 0, bm = 0, bo = 0;
+    for (uint32_t i = 0; i < wv; ++i) {
+        bc += L.wsum[0][i];
+        bm = max(bm, L.wsum[1][i]);
+        bo += L.wsum[2][i];
+    }
+    uint32_t xc = bc + ic - c, xm = max(bm, __shfl_up(im, 1) * (lane ? 1u : 0u)), xo = bo + io - o;  // exclusive
+#pragma unroll
+    for (uint32_t k = 0; k < kPerThr; ++k) {
+        const uint32_t sg = t * kPerThr + k;
+        if (sg < K.nseg) {
+            L.rbase[sg] = xc;
+            L.prev_end[sg] = xm;
+            L.obase[sg] = xo;
+        }
+        xc += nr[k];
+        xm = max(xm, en[k]);
+        xo += ob[k];
+    }
+    if (t == kBlkThreads - 1) {
+        L.rbase[K.nseg] = xc;
+        L.total = xm;  // the last match's end: the final literal run starts here
+        L.obase[K.nseg] = xo;
     }
     __syncthreads();
 }
@@ -639,24 +691,29 @@ __device__ __forceinline__ uint32_t seg_of(const BlkLds &L, uint32_t nseg, uint3
 __global__ __launch_bounds__(kBlkThreads) void k_lz4_size(const Batch B)
 {
     __shared__ BlkLds L;
-    __shared__ uint64_t s_sum[kBlkThreads / 64];
     const Blk K = B.blks[blockIdx.x];
-    blk_prologue(B, K, L);
+    for (uint32_t i = threadIdx.x; i < K.nseg; i += kBlkThreads) L.acc[i] = 0;
+    blk_prologue(B, K, L, false);
     const uint32_t nr = L.rbase[K.nseg];
     const uint32_t last_end = uint32_t(L.total);
-    uint64_t sum = 0;
     for (uint32_t r = threadIdx.x; r < nr; r += kBlkThreads) {
-        const uint32_t s = seg_of(L, K.nseg, r);
+        const uint32_t sg = seg_of(L, K.nseg, r);
         uint32_t ls, ll, mp, off, ml;
-        rec_geom(B, K, L, s, r - L.rbase[s], ls, ll, mp, off, ml);
-        sum += seq_size(ll, ml);
+        rec_geom(B, K, L, sg, r - L.rbase[sg], ls, ll, mp, off, ml);
+        atomicAdd(&L.acc[sg], seq_size(ll, ml));
+    }
+    __syncthreads();
+    uint32_t sum = 0;
+    for (uint32_t i = threadIdx.x; i < K.nseg; i += kBlkThreads) {
+        B.seg_out[K.seg0 + i] = L.acc[i];
+        sum += L.acc[i];
     }
     for (int o = 32; o; o >>= 1) sum += __shfl_xor(sum, o);
-    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = sum;
+    if ((threadIdx.x & 63) == 0) L.wsum[0][threadIdx.x >> 6] = sum;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t t = 0;
-        for (uint32_t i = 0; i < kBlkThreads / 64; ++i) t += s_sum[i];
+        for (uint32_t i = 0; i < kBlkThreads / 64; ++i) t += L.wsum[0][i];
         const uint32_t fl = K.len - last_end;
         t += 1 + ext_len(fl) + fl;
         B.blk_size[blockIdx.x] = t < K.len ? uint32_t(t) : (K.len | 0x80000000u);
@@ -793,7 +850,8 @@ __global__ __launch_bounds__(256) void k_copy(const Batch B)
 }
 
 // Grid (blocks, kEmitSplit): a stored block is copied by all its kEmitSplit
-// workgroups, a compressed one written by the first.
+// workgroups, a compressed one written by segment ranges, one per workgroup
+// (its output offset from k_lz4_size's per-segment sizes).
 constexpr uint32_t kEmitSplit = 16;
 
 __global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
@@ -817,22 +875,22 @@ __global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
         copy_span(dst + a, src + a, e - a, threadIdx.x, kBlkThreads);
         return;
     }
-    if (blockIdx.y) return;
-    blk_prologue(B, K, L);
-    const uint32_t nr = L.rbase[K.nseg];
+    // compressed: workgroup y writes the sequences of segments [sa, sb)
+    blk_prologue(B, K, L, true);
+    const uint32_t sa = K.nseg * blockIdx.y / kEmitSplit, sb = K.nseg * (blockIdx.y + 1) / kEmitSplit;
+    const uint32_t r0 = L.rbase[sa], r1 = L.rbase[sb];
     const uint32_t last_end = uint32_t(L.total);
-    // tiles of kBlkThreads records: sizes, block-wide exclusive scan, write
+    // tiles of kBlkThreads records: sizes, workgroup-wide exclusive scan, write
     __shared__ uint32_t s_part[kBlkThreads / 64];
-    uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < nr; t0 += kBlkThreads) {
+    uint32_t carry = L.obase[sa];
+    for (uint32_t t0 = r0; t0 < r1; t0 += kBlkThreads) {
         const uint32_t r = t0 + threadIdx.x;
         uint32_t ls = 0, ll = 0, mp = 0, off = 0, ml = 0, sz = 0;
-        if (r < nr) {
-            const uint32_t s = seg_of(L, K.nseg, r);
-            rec_geom(B, K, L, s, r - L.rbase[s], ls, ll, mp, off, ml);
+        if (r < r1) {
+            const uint32_t sg = seg_of(L, K.nseg, r);
+            rec_geom(B, K, L, sg, r - L.rbase[sg], ls, ll, mp, off, ml);
             sz = seq_size(ll, ml);
         }
-        // exclusive scan of sz over the workgroup
         uint32_t x = sz;
         const uint32_t lane = threadIdx.x & 63u;
         for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -846,7 +904,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
         uint32_t tile_total = 0;
         for (uint32_t i = 0; i < kBlkThreads / 64; ++i) tile_total += s_part[i];
         __syncthreads();
-        if (r < nr) {
+        if (r < r1) {
             uint8_t *o = dst + carry + wbase + x - sz;
             const uint32_t lt = ll >= 15 ? 15 : ll, mt = ml - 4 >= 15 ? 15 : ml - 4;
             *o++ = uint8_t(lt << 4 | mt);
@@ -867,8 +925,8 @@ __global__ __launch_bounds__(kBlkThreads) void k_lz4_emit(const Batch B)
         }
         carry += tile_total;
     }
-    if (threadIdx.x == 0) {  // the final literal-only sequence
-        uint8_t *o = dst + carry;
+    if (threadIdx.x == 0 && sb == K.nseg) {  // the final literal-only sequence
+        uint8_t *o = dst + L.obase[K.nseg];
         const uint32_t ll = K.len - last_end;
         *o++ = uint8_t((ll >= 15 ? 15 : ll) << 4);
         if (ll >= 15) {
@@ -1384,7 +1442,8 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     };
     const size_t o_blobs = take(nb * sizeof(BlobDesc)), o_blks = take(nk * sizeof(Blk)), o_segs = take(ng * sizeof(Seg));
     const size_t o_rnd = take(encrypt ? nb * 56 : 0), o_key = take(32);
-    const size_t o_recs = take(ng * kRecCap * sizeof(uint2)), o_nrec = take(ng * 4), o_trail = take(ng * 4);
+    const size_t o_recs = take(ng * kRecCap * sizeof(uint2)), o_nrec = take(ng * 4), o_trail = take(ng * 4),
+                 o_sout = take(ng * 4);
     const size_t o_bsz = take(nk * 4), o_bfo = take(nk * 8), o_xxh = take(nb * 4), o_flen = take(nb * 8);
     const size_t o_oo = take((nb + 1) * 8), o_pb = take((nb + 1) * 4), o_keys = take(encrypt ? nb * sizeof(BlobKey) : 0);
     const size_t o_status = take(8), o_frames = take(encrypt ? slot : 0), o_xx = take(compress ? nb * 4 : 0);
@@ -1422,6 +1481,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     Bt.recs = reinterpret_cast<uint2 *>(ws + o_recs);
     Bt.nrec = reinterpret_cast<uint32_t *>(ws + o_nrec);
     Bt.trail = reinterpret_cast<uint32_t *>(ws + o_trail);
+    Bt.seg_out = reinterpret_cast<uint32_t *>(ws + o_sout);
     Bt.blk_size = reinterpret_cast<uint32_t *>(ws + o_bsz);
     Bt.blk_foff = reinterpret_cast<uint64_t *>(ws + o_bfo);
     Bt.xxh = reinterpret_cast<uint32_t *>(ws + o_xxh);
