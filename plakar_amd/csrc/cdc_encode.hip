@@ -282,8 +282,6 @@ struct Batch {
     const uint32_t *xx_ids;   // XXH32 order of the blobs
 };
 
-constexpr uint32_t kNoneU32 = 0xFFFFFFFFu;
-
 // Global-memory views (global_load, counted in vmcnt only; a generic pointer
 // gives flat loads, which also count in lgkmcnt).
 typedef __attribute__((address_space(1))) const uint32_t gu32;
@@ -351,7 +349,6 @@ __global__ __launch_bounds__(kXxWaves * 64) void k_xxh32(const Batch B)
     uint32_t lw, cw;
     blob(lg, lp, ln, lw);
     blob(cg < kXxPerWave ? cg : 0u, cp, cn, cw);
-    const uint64_t lnw = ln / 16 * 4;  // words in the loaded blob's stripes
     const uint64_t cstripes = cg < kXxPerWave ? cn / 16 : 0;
     // a global-address-space pointer: flat loads would also count in
     // lgkmcnt, so every LDS wait of the chains would wait for the prefetch too
