@@ -172,3 +172,23 @@ def test_backup_batch_device_encoder():
             assert hashlib.sha256(plain).digest() == c
             seen += 1
     assert seen == len({c.Checksum for ob in objs for c in ob.Chunks})
+
+
+def test_encode_device_offsets_across_tensors():
+    """Offsets are plain device-address displacements from d_base, so one call
+    can cover the chunks of several device buffers (bench.py's encode leg)."""
+    parts = [low_entropy(3 << 20, 41), random_bytes((2 << 20) + 333, 42)]
+    ts = [torch.from_numpy(p).cuda() for p in parts]
+    base = min(ts, key=lambda t: t.data_ptr())
+    offs, lens, src = [], [], []
+    for p, t in zip(parts, ts):
+        for a, n in ((0, 70_000), (70_000, 1_000_001), (1_070_001, p.size - 1_070_001)):
+            offs.append(t.data_ptr() - base.data_ptr() + a)
+            lens.append(n)
+            src.append(p[a:a + n].tobytes())
+    cap = sum(encode.encode_bound(n) for n in lens)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    oo = encode.encode_device(base, offs, lens, out, key=KEY)
+    host = out.cpu().numpy()
+    for i, s in enumerate(src):
+        assert ref.decode(host[oo[i]:oo[i + 1]].tobytes(), key=KEY) == s
