@@ -273,39 +273,62 @@ def encode_leg(torch, batch, bufs, reps, baseline):
     return d
 
 
-def chunk_digest_pipeline(torch, bufs, opts, dev, nstreams, passes):
+def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
     """Chunking + per-chunk SHA-256 and histograms (processChunk's device work,
-    snapshot/backup.go:594-629) as a backup streams batches: each pass chunks
-    the rank's buffers, then hashes every chunk, on its own stream; `nstreams`
-    passes are in flight at once, so one pass's digests (a serial chain per
-    chunk: the longest chunk sets a launch's time) overlap the next passes'
-    chunking and digests.  Combined GiB/s of input bytes; not part of `value`."""
+    snapshot/backup.go:594-629) as a backup streams batches: passes chunk the
+    rank's buffers on two alternating streams, and every `window` passes one
+    digest launch group on a third stream hashes the chunks of those passes
+    (a window's cut lists stay in HBM until their digests are done; two
+    windows alternate, so chunking runs ahead while the previous window
+    hashes).  Hashing a window at once is what fills the device: a SHA-256
+    chain is serial per chunk, so a launch needs many chunks in flight (one
+    C1 pass has ~11 K, the device keeps ~65 K lanes resident).  Combined GiB/s
+    of input bytes; not part of `value`."""
     from plakar_amd import device as devmod
     from plakar_amd import hashing
-    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
-    batches = [devmod.DeviceBatch(bufs, opts, final=True, device=dev.index) for _ in range(nstreams)]
+    cstreams = [torch.cuda.Stream(dev) for _ in range(2)]
+    dstreams = [torch.cuda.Stream(dev) for _ in range(4)]
+    sets = [[devmod.DeviceBatch(bufs, opts, final=True, device=dev.index) for _ in range(window)] for _ in range(2)]
+    chunked = [[torch.cuda.Event() for _ in range(window)] for _ in range(2)]
+    hashed = [[], []]
+    wbufs = [t for _ in range(window) for t in bufs]
+    per = 32  # buffers per digest launch group (cdc_chunk_digests_device_batch_async splits there)
 
-    def one(i):
-        s = streams[i % nstreams]
-        b = batches[i % nstreams]
-        b.launch(s)
-        cut_lists = [b.cuts[k] for k in range(b.n)]
-        with torch.cuda.stream(s):
-            hashing.chunk_digests_batch(bufs, cut_lists, [b.res[k] for k in range(b.n)], stream=s)
-    for i in range(nstreams):  # warm-up
-        one(i)
+    def one_round(r):
+        w = r % 2
+        for i in range(window):
+            s = cstreams[i % 2]
+            if i < 2:  # the set's previous digests are done with its cut lists
+                for e in hashed[w]:
+                    s.wait_event(e)
+            sets[w][i].launch(s)
+            chunked[w][i].record(s)
+        cuts = [b.cuts[k] for b in sets[w] for k in range(b.n)]
+        res = [b.res[k] for b in sets[w] for k in range(b.n)]
+        hashed[w] = []
+        for g in range(0, len(wbufs), per):  # launch groups alternate over the digest streams
+            ds = dstreams[(g // per) % len(dstreams)]
+            for e in chunked[w]:
+                ds.wait_event(e)
+            with torch.cuda.stream(ds):
+                hashing.chunk_digests_batch(wbufs[g:g + per], cuts[g:g + per], res[g:g + per], stream=ds)
+            ev = torch.cuda.Event()
+            ev.record(ds)
+            hashed[w].append(ev)
+    for r in range(2):  # warm-up
+        one_round(r)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(passes):
-        one(i)
+    for r in range(rounds):
+        one_round(r)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    passes = rounds * window
     total = sum(t.numel() for t in bufs) * passes
-    return dict(value=round(total / el / GIB, 2), unit="GiB/s", streams=nstreams, passes=passes,
+    return dict(value=round(total / el / GIB, 2), unit="GiB/s", window=window, passes=passes,
                 ms_per_pass=round(el / passes * 1e3, 3),
-                bound="digest kernel occupancy: each pass's chunks in flight x the per-64-B-block latency of one "
-                      "SHA-256 chain (~1.9 us at one wave per SIMD); LDS (64 KiB per digest workgroup) caps "
-                      "concurrent passes")
+                bound="SHA-256 lanes resident (two 128-lane workgroups per CU) x the per-64-B-block time of a "
+                      "chain; the window's longest chunk run sets its launch's tail")
 
 
 def cpu_baseline(bufs_host, cuts_dev, opts, seconds, threads=1):
@@ -383,8 +406,8 @@ def main():
                     help="Encode leg (LZ4 frame + AES-256-GCM of every chunk, not part of value); 0 disables")
     ap.add_argument("--digest-reps", type=int, default=3,
                     help="reps of the per-chunk SHA-256 + histogram leg (SURVEY.md 8f; 0 = skip)")
-    ap.add_argument("--digest-streams", type=int, default=4,
-                    help="passes in flight in the pipelined chunk + digest leg")
+    ap.add_argument("--digest-window", type=int, default=8,
+                    help="passes per digest launch in the pipelined chunk + digest leg")
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="reps of the PCIe-inclusive host-buffer leg (0 = skip)")
     args = ap.parse_args()
@@ -531,8 +554,7 @@ def main():
     digest = None
     if not host_mode and args.digest_reps > 0:
         digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0 and world == 1)
-        digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_streams,
-                                                                  max(args.digest_streams * 2, 8))
+        digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_window, 4)
 
     encode_res = None
     if not host_mode and args.encode_reps > 0:

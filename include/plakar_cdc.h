@@ -322,6 +322,14 @@ int cdc_set_maskl_index_mode(int mode);
  * group needed it), *groups = launch groups issued on the device so far.  Not a reference interface. */
 int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups);
 
+/* Per-chunk digests: the lane count the digest kernels assume the device
+ * keeps resident (a launch with more chunks than this gives each lane a run
+ * of ceil(chunks / lanes) consecutive chunks).  0 (the default) derives it
+ * from the device's CU count; tests set small values to cover multi-chunk
+ * lanes on small inputs.  Digests never depend on it.  Not a reference
+ * interface.  Returns CDC_OK. */
+int cdc_debug_set_digest_lanes(uint64_t lanes);
+
 /* Live profiling of the device path: when enabled, every launch group records
  * hipEvents on its stream before/after the scan kernel and after the last
  * resolution kernel.  collect() waits for the recorded events, returns the

@@ -10,7 +10,7 @@ import warnings
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PLAKAR_CDC_LIB selects an alternative build of the same library (kernel
-# variants for A/B measurements, tools/variants.sh); default: the in-tree build.
+# variants for A/B measurements, tools/ab.sh); default: the in-tree build.
 LIB_PATH = os.environ.get("PLAKAR_CDC_LIB") or os.path.join(_HERE, "_lib", "libplakar_cdc.so")
 
 CDC_OK = 0
@@ -138,6 +138,7 @@ SIGNATURES = {
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_debug_maskl_state": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_uint32), _P(ctypes.c_uint64)]),
+    "cdc_debug_set_digest_lanes": (ctypes.c_int, [ctypes.c_uint64]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),
                                            _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),

@@ -28,19 +28,22 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force=False, verbose=True):
-    if not force and not _stale(LIB, SOURCES + HEADERS):
-        return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB + ".tmp"
+def build_lib(force=False, verbose=True, out=None, defines=()):
+    """Build the library (out: another path for an experiment variant,
+    defines: extra -D flags for it)."""
+    target = out or LIB
+    if not force and not defines and not _stale(target, SOURCES + HEADERS):
+        return target
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    tmp = target + ".tmp"
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function",
-           "-o", tmp] + SOURCES
+           "-o", tmp] + [f"-D{d}" for d in defines] + SOURCES
     if verbose:
         print("[plakar_amd.build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, target)
+    return target
 
 
 def build_oracle(verbose=True):

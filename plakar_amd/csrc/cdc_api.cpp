@@ -646,6 +646,12 @@ int cdc_set_maskl_index_mode(int mode)
     return CDC_OK;
 }
 
+int cdc_debug_set_digest_lanes(uint64_t lanes)
+{
+    cdc::g_digest_lanes = lanes;
+    return CDC_OK;
+}
+
 int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups)
 {
     if (!hint || !groups) return CDC_E_INVALID;

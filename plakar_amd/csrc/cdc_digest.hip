@@ -17,6 +17,8 @@
 // SIMD; a launch lasts as long as its longest chunk.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "cdc_internal.h"
 
 namespace cdc {
@@ -37,24 +39,24 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU
 }
 
-// Two or three waves per workgroup of 64 chunks, one lane per chunk in each:
-//   wave 1, the producer: loads block b + 1's words while it works on block b,
-//     builds the big-endian words (v_perm funnel shift + byte swap), pads the
+// SHA-256: two waves per group of 64 lanes; a lane hashes a run of
+// consecutive chunks of the cut list, one after the other (one chunk per lane
+// unless the launch holds more chunks than the device keeps lanes resident),
+// taking its next chunk from its workgroup's queue, so every resident lane
+// stays busy until the launch drains instead of idling once its one chunk is
+// done.  Per lane:
+//   the producer: loads block b + 2's words while it works on block b
+//     (across chunk boundaries: the next chunk's first blocks), builds the
+//     big-endian words (v_perm funnel shift + byte swap), pads each chunk's
 //     final block(s) and expands the message schedule W[0..63] into an LDS
 //     ring stage;
-//   wave 2 (histograms requested): the same words, counted;
-//   wave 0, the consumer: the 64 rounds of block b - 1 from the other stage.
+//   the consumer: the 64 rounds of block b - 1 from the other stage, the
+//     digest written when a chunk's last block is done.
 // One s_barrier per block.  The consumer's chain is ~14 VALU per round
-// instead of ~25 when one lane did everything; the producer's ~560 VALU and
-// the counter's ~160 VALU + 64 LDS atomics fit under it on other SIMDs.
+// instead of ~25 when one lane did everything; the producer's ~560 VALU fit
+// under it on another SIMD.
 constexpr uint32_t kShaRing = 2;                                   // stages
 constexpr uint32_t kRingBytes = kShaRing * 64u * 64u * 4u;         // 32 KiB: [stage][word quad][lane] uint4
-// The histogram: u16 halves, lanes l and l + 32 share the dword of bin b at
-// 4 * (32 b + (l & 31)) (every access of a wave stays in its own bank pair),
-// 32 KiB; flushed to the u32 output every kFlushBlocks blocks so that a half
-// never passes 64 x 1023 < 65536 counts.
-constexpr uint32_t kHistPairBytes = 256u * 32u * 4u;
-constexpr uint64_t kFlushBlocks = 1023;
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v)
 {
@@ -63,158 +65,246 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     return v;
 }
 
-template <bool HIST>
-__global__ __launch_bounds__(192) void k_chunk_digest(const DigestBatch DB)
+__device__ __forceinline__ uint64_t chunk_count(const DigestBuf &B)
 {
-    extern __shared__ uint4 s_mem[];
-    uint4 *ring = s_mem;                                                   // [kShaRing][16][64]
-    uint32_t *s_hist = reinterpret_cast<uint32_t *>(s_mem + kShaRing * 16 * 64);  // [256][32]
+    return B.res ? min<uint64_t>(B.cap, uint64_t(B.res->ncuts)) : B.cap;
+}
+
+// Cut c, clipped to the buffer (a malformed list must not fault).
+__device__ __forceinline__ void cut_at(const DigestBuf &B, uint64_t c, uint64_t &off, uint64_t &n)
+{
+    const cdc_cut cut = B.cuts[c];
+    off = cut.offset;
+    n = cut.length;
+    if (off > B.len) n = 0;
+    else if (n > B.len - off) n = B.len - off;
+}
+
+// blocks of the padded message: the full ones, then 1 or 2
+__device__ __forceinline__ uint64_t sha_blocks(uint64_t n) { return n / 64u + ((n % 64u) <= 55u ? 1u : 2u); }
+
+// A chunk's bytes as aligned dwords: q[0] holds its first byte at byte sh,
+// block b uses q[16 b .. 16 b + 16] (funnel-shifted by sel), q[lastq] holds
+// its last byte.
+struct ChunkWords {
+    const uint32_t *q;
+    uint32_t sel;
+    uint64_t lastq;
+};
+
+__device__ __forceinline__ ChunkWords chunk_words(const uint8_t *data, uint64_t off, uint64_t n)
+{
+    const uint8_t *p = data + off;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+    return ChunkWords{reinterpret_cast<const uint32_t *>(p - sh),
+                      (sh << 24) | ((sh + 1u) << 16) | ((sh + 2u) << 8) | (sh + 3u), n ? (sh + n - 1u) >> 2 : 0};
+}
+
+// block b's 16 dwords after q[16 b]; clamped to lastq near the end (bytes from
+// past it are masked off by the padding)
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-B loads
+
+__device__ __forceinline__ void load16(const ChunkWords &A, uint64_t b, uint32_t (&x)[16])
+{
+    const uint64_t base = 16u * b + 1u;
+    if (base + 15u <= A.lastq) {  // four dwordx4 loads (a lane's own chunk: 4x fewer per-lane line lookups)
+        const u32x4_a4 *qb = reinterpret_cast<const u32x4_a4 *>(A.q + base);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x4_a4 v = qb[k];
+            x[4 * k] = v.x;
+            x[4 * k + 1] = v.y;
+            x[4 * k + 2] = v.z;
+            x[4 * k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = A.q[min<uint64_t>(base + k, A.lastq)];
+    }
+}
+
+// Two lane groups of 64 per workgroup (two workgroups per CU by LDS), waves
+// by role so that a SIMD runs one round wave: a workgroup's waves land on
+// SIMDs in the cyclic order 0 -> 2 -> 1 -> 3 (MI355X_MICROARCH.md, LDS;
+// tools/wave_place.hip), so waves 0-1 (the producers) and 2-3 (the rounds)
+// sit on four SIMDs.
+#ifndef CDC_DIGEST_GROUPS
+#define CDC_DIGEST_GROUPS 2
+#endif
+constexpr uint32_t kDigestGroups = CDC_DIGEST_GROUPS;
+constexpr uint32_t kDigestWaves = 2 * kDigestGroups;
+
+// Per-lane block metadata beside each ring stage (written by the producer,
+// read by the rounds one block behind): the chunk (relative to the
+// workgroup's first) and flags.
+constexpr uint32_t kMetaLive = 1u << 9, kMetaLast = 1u << 10;  // bits 0-8: rb + 128
+
+__global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const DigestBatch DB)
+{
+    constexpr uint32_t kLanes = 64u * kDigestGroups;
+    __shared__ uint4 s_ring[kDigestGroups][kRingBytes / 16u];
+    __shared__ uint32_t s_meta[kDigestGroups][kShaRing][2][64];
+    __shared__ uint32_t s_any[kShaRing][kDigestGroups];  // some lane of the group holds a block in that stage
+    __shared__ uint32_t s_next;                          // the workgroup's chunk queue (relative)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t grp = wave % kDigestGroups;
+    const uint32_t role = wave / kDigestGroups;  // 0 producer, 1 rounds
+    uint4 *ring = s_ring[grp];                   // [kShaRing][16][64]
     const DigestBuf &B = DB.b[blockIdx.y];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 rounds, 1 schedule, 2 histogram
-    uint64_t n_cuts = B.cap;
-    if (B.res) n_cuts = min<uint64_t>(B.cap, uint64_t(B.res->ncuts));
-    if (uint64_t(blockIdx.x) * 64u >= n_cuts) return;  // whole workgroup: no barrier is left waiting
-    const uint64_t i = uint64_t(blockIdx.x) * 64u + lane;
-    const bool valid = i < n_cuts;
-    uint64_t n = 0, off = 0;
-    if (valid) {
-        const cdc_cut cut = B.cuts[i];
-        off = cut.offset;
-        n = cut.length;
-        if (off > B.len) n = 0;
-        else if (n > B.len - off) n = B.len - off;  // clipped to the buffer (a malformed list must not fault)
-    }
-    // blocks of the padded message: the full ones, then 1 or 2
-    const uint64_t nb = valid ? n / 64u + ((n % 64u) <= 55u ? 1u : 2u) : 0u;
-    const uint64_t NB = wave_max(uint32_t(min<uint64_t>(nb, 0xFFFFFFFFull)));  // both waves: same lanes, same bound
+    // Chunks per workgroup: kLanes while the launch fits the resident lanes,
+    // else kLanes * k, k = ceil(chunks / resident lanes) (every wave of every
+    // workgroup derives the same k).  The workgroup's lanes take its chunks
+    // in order from an LDS queue, a lane its next one block before its
+    // current one's last.
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < DB.nbufs; ++j) total += chunk_count(DB.b[j]);
+    const uint64_t R = DB.resident_lanes ? DB.resident_lanes : 1u;
+    const uint64_t k = total > R ? (total + R - 1) / R : 1u;
+    const uint64_t n_cuts = chunk_count(B);
+    const uint64_t C0 = uint64_t(blockIdx.x) * kLanes * k;
+    if (C0 >= n_cuts) return;  // whole workgroup: no barrier is left waiting
+    const uint64_t C1 = min(C0 + kLanes * k, n_cuts);
+    if (threadIdx.x == 0) s_next = kLanes;
+    __syncthreads();
 
-    if (role != 0) {
-        const bool counting = HIST && role == 2;  // uniform per wave
-        const uint8_t *p = B.data + (valid ? off : 0);
-        const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
-        const uint32_t sel = (sh << 24) | ((sh + 1u) << 16) | ((sh + 2u) << 8) | (sh + 3u);
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(p - sh);
-        const uint64_t lastq = n ? (sh + n - 1u) >> 2 : 0;  // last dword holding a byte of the chunk
-        const uint32_t hoff = (lane & 31u) * 4u, hinc = 1u << (16u * (lane >> 5));
-        if (counting) {
-#pragma unroll 8
-            for (uint32_t b = 0; b < 256; b += 2) s_hist[b * 32u + lane] = 0;  // 64 lanes, two bins a step
+    if (role == 0) {
+        // Blocks are loaded two ahead of the one being scheduled (a lane's
+        // loads are uncoalesced and one block of cover left the producer
+        // waiting on memory).  Every slot issues the same 17 dword loads on
+        // every path (clamped to the chunk's last dword; a lane without a
+        // block reads the cut list), so the compiler's vmcnt waits only for
+        // the slot it consumes.
+        const uint32_t *dummy = reinterpret_cast<const uint32_t *>(B.cuts);
+        uint64_t lc = C0 + 64u * grp + lane, loff = 0, ln = 0, lnb = 0, lb = 0;  // load cursor
+        bool lhas = lc < C1;
+        if (lhas) {
+            cut_at(B, lc, loff, ln);
+            lnb = sha_blocks(ln);
         }
-        auto count1 = [&](uint32_t byte) {
-            __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(s_hist) + ((byte << 7) | hoff)),
-                                   hinc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ChunkWords LA = chunk_words(B.data, loff, ln);
+        // the load cursor's next chunk, taken from the queue (and its cut
+        // loaded) one block before the current one's last: late enough that
+        // a lane does not hold a chunk it will only start much later (the
+        // launch's tail), early enough to hide the cut's load
+        uint64_t cn = ~0ull, noff = 0, nn = 0;
+        bool resv = false;
+        auto reserve = [&]() {
+            cn = C0 + __hip_atomic_fetch_add(&s_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cn < C1) cut_at(B, cn, noff, nn);
+            else cn = ~0ull;
+            resv = true;
         };
-        bool flushed = false;
-        auto flush = [&]() {
-            if (valid && B.hist) {
-                uint4 *ho = reinterpret_cast<uint4 *>(B.hist + i * 256u);
-                const uint32_t hs = 16u * (lane >> 5);
-#pragma unroll 4
-                for (uint32_t b = 0; b < 256; b += 4) {
-                    uint4 v = make_uint4((s_hist[b * 32u + (lane & 31u)] >> hs) & 0xFFFFu,
-                                         (s_hist[(b + 1) * 32u + (lane & 31u)] >> hs) & 0xFFFFu,
-                                         (s_hist[(b + 2) * 32u + (lane & 31u)] >> hs) & 0xFFFFu,
-                                         (s_hist[(b + 3) * 32u + (lane & 31u)] >> hs) & 0xFFFFu);
-                    if (flushed) {
-                        const uint4 o = ho[b / 4];
-                        v = make_uint4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
+        struct Blk {
+            uint32_t x[17];  // q[16 b .. 16 b + 16]
+            uint32_t sel, crel, n, itc;
+            bool live;
+        };
+        auto issue = [&](Blk &k) {  // the load cursor's block into k, then advance the cursor
+            const bool real = lhas && ln != 0;
+            const uint32_t *q = real ? LA.q : dummy;
+            const uint64_t base = real ? 16u * lb : 0u, lim = real ? LA.lastq : 0u;
+#pragma unroll
+            for (int j = 0; j < 17; ++j) k.x[j] = q[min<uint64_t>(base + j, lim)];
+            k.live = lhas;
+            k.sel = LA.sel;
+            k.crel = uint32_t(lc - C0);
+            k.n = uint32_t(ln);
+            k.itc = uint32_t(lb);
+            if (lhas) {
+                ++lb;
+                if (!resv && lb + 1u >= lnb) reserve();
+                if (lb == lnb) {
+                    if (cn != ~0ull) {
+                        lc = cn;
+                        loff = noff;
+                        ln = nn;
+                        lnb = sha_blocks(nn);
+                        lb = 0;
+                        LA = chunk_words(B.data, loff, ln);
+                        resv = false;
+                    } else {
+                        lhas = false;
                     }
-                    ho[b / 4] = v;
                 }
             }
-#pragma unroll 8
-            for (uint32_t b = 0; b < 256; b += 2) s_hist[b * 32u + lane] = 0;
-            flushed = true;
         };
-        // block b uses dwords q[16 b .. 16 b + 16]; the loads are clamped to
-        // lastq near the end (bytes from past it are masked off below)
-        auto load16 = [&](uint64_t b, uint32_t (&x)[16]) {
-            const uint64_t base = 16u * b + 1u;
-            if (base + 15u <= lastq) {
-                const uint32_t *qb = q + base;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) x[k] = qb[k];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) x[k] = q[min<uint64_t>(base + k, lastq)];
-            }
-        };
-        uint32_t lo = 0, nx[16];
-        if (n) {
-            lo = q[0];
-            load16(0, nx);
-        }
-        for (uint64_t it = 0; it < NB; ++it) {
+        // schedule block `it` from slot k; false once no lane of the workgroup has one
+        auto step = [&](uint32_t it, const Blk &k) -> bool {
+            const bool live = k.live;
+            const bool last = live && k.itc + 1u == sha_blocks(k.n);  // the chunk's final block
             uint32_t w[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                w[k] = __builtin_amdgcn_perm(nx[k], lo, sel);
-                lo = nx[k];
-            }
-            if (n && it + 1 < nb) load16(it + 1, nx);  // next block's words, in flight during this one
-            const int64_t rb64 = int64_t(n) - int64_t(64u * it);  // bytes of the chunk from this block on
-            const int32_t rb = int32_t(max<int64_t>(-128, min<int64_t>(128, rb64)));
-            if (counting && rb >= 64) {
+            for (int q = 0; q < 16; ++q) w[q] = __builtin_amdgcn_perm(k.x[q + 1], k.x[q], k.sel);
+            const int64_t rb64 = int64_t(k.n) - int64_t(64u * k.itc);  // bytes of the chunk from this block on
+            const int32_t rb = live ? int32_t(max<int64_t>(-128, min<int64_t>(128, rb64))) : 128;
+            if (rb < 64 && rb > -64) {  // the chunk's final block or two: data bytes, 0x80, zeros, bit length
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    count1(w[k] >> 24);
-                    count1(__builtin_amdgcn_ubfe(w[k], 16, 8));
-                    count1(__builtin_amdgcn_ubfe(w[k], 8, 8));
-                    count1(w[k] & 0xFFu);
-                }
-            }
-            if (rb < 64 && rb > -64) {  // the lane's final block or two: data bytes, 0x80, zeros, bit length
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int32_t rem = rb - 4 * k;
+                for (int q = 0; q < 16; ++q) {
+                    const int32_t rem = rb - 4 * q;
                     const uint32_t keep = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * rem));
                     const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
-                    w[k] = (w[k] & keep) | pad;
-                    if (counting) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (j < rem) count1((w[k] >> (24 - 8 * j)) & 0xFFu);
-                    }
+                    w[q] = (w[q] & keep) | pad;
                 }
                 if (rb <= 55) {
-                    const uint64_t bits = n * 8u;
+                    const uint64_t bits = uint64_t(k.n) * 8u;
                     w[14] = uint32_t(bits >> 32);
                     w[15] = uint32_t(bits);
                 }
             }
-            if (!counting) {
-                uint4 *st = ring + (it & 1u) * 1024u + lane;
+            const uint32_t stg = it & 1u;
+            uint4 *st = ring + stg * 1024u + lane;
 #pragma unroll
-                for (int k = 0; k < 16; k += 4) st[k * 16] = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
-                uint32_t x4[4];
+            for (int q = 0; q < 16; q += 4) st[q * 16] = make_uint4(w[q], w[q + 1], w[q + 2], w[q + 3]);
+            uint32_t x4[4];
 #pragma unroll
-                for (int t = 16; t < 64; ++t) {
-                    const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-                    const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
-                    const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-                    const uint32_t wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
-                    w[t & 15] = wt;
-                    x4[t & 3] = wt;
-                    if ((t & 3) == 3) st[(t / 4) * 64] = make_uint4(x4[0], x4[1], x4[2], x4[3]);
-                }
+            for (int t = 16; t < 64; ++t) {
+                const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+                const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+                const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+                const uint32_t wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+                w[t & 15] = wt;
+                x4[t & 3] = wt;
+                if ((t & 3) == 3) st[(t / 4) * 64] = make_uint4(x4[0], x4[1], x4[2], x4[3]);
             }
-            if (counting && (it + 1) % kFlushBlocks == 0) flush();
+            s_meta[grp][stg][0][lane] = k.crel;
+            s_meta[grp][stg][1][lane] = uint32_t(rb + 128) | (live ? kMetaLive : 0u) | (last ? kMetaLast : 0u);
+            const bool any = __ballot(live) != 0;
+            if (lane == 0) s_any[stg][grp] = any ? 1u : 0u;
             __syncthreads();
+            return (s_any[stg][0] | s_any[stg][kDigestGroups - 1]) != 0;  // every wave stops after the same barrier
+        };
+        Blk b0, b1, b2;
+        issue(b0);
+        issue(b1);
+        for (uint32_t it = 0;; it += 3) {  // unrolled by the slot rotation
+            issue(b2);
+            if (!step(it, b0)) break;
+            issue(b0);
+            if (!step(it + 1, b1)) break;
+            issue(b1);
+            if (!step(it + 2, b2)) break;
         }
-        __syncthreads();  // the consumer's last block
-        if (counting) flush();
-    } else {
-        uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                         0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    } else {  // role 1: the rounds
+        constexpr uint32_t kIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                     0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+        uint32_t h[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = kIV[j];
         __builtin_amdgcn_s_setprio(3);  // the critical chain wins issue when waves share a SIMD
-        __syncthreads();  // stage 0 filled
-        for (uint64_t it = 0; it < NB; ++it) {
-            const uint4 *st = ring + (it & 1u) * 1024u + lane;
-            uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+        for (uint32_t it = 0;; ++it) {
+            __syncthreads();  // stage it filled
+            const uint32_t stg = it & 1u;
+            // the stop flag, the block's metadata and its first words in one round trip
+            const uint32_t any = s_any[stg][0] | s_any[stg][kDigestGroups - 1];
+            const uint32_t m = s_meta[grp][stg][1][lane], crel = s_meta[grp][stg][0][lane];
+            const uint4 *st = ring + stg * 1024u + lane;
+            const uint4 v0 = st[0];
+            if (!any) break;
+            uint32_t a = h[0], b = h[1], cc = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
 #pragma unroll
             for (int q4 = 0; q4 < 16; ++q4) {
-                const uint4 v = st[q4 * 64];
+                const uint4 v = q4 ? st[q4 * 64] : v0;
                 const uint32_t wq[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -223,37 +313,102 @@ __global__ __launch_bounds__(192) void k_chunk_digest(const DigestBatch DB)
                     const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
                     const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wq[j];
                     const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-                    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+                    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, cc, 0xE8);
                     hh = g;
                     g = f;
                     f = e;
                     e = d + t1;
-                    d = c;
-                    c = b;
+                    d = cc;
+                    cc = b;
                     b = a;
                     a = t1 + S0 + mj;
                 }
             }
-            if (it < nb) {
+            if (m & kMetaLive) {
                 h[0] += a;
                 h[1] += b;
-                h[2] += c;
+                h[2] += cc;
                 h[3] += d;
                 h[4] += e;
                 h[5] += f;
                 h[6] += g;
                 h[7] += hh;
+                if (m & kMetaLast) {  // the chunk's digest, then the next chunk from the IV
+                    uint4 *out = reinterpret_cast<uint4 *>(B.digests + (C0 + crel) * 32u);
+                    auto bswap = [](uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); };
+                    out[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
+                    out[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) h[j] = kIV[j];
+                }
             }
-            __syncthreads();
-        }
-        if (valid) {
-            uint4 *out = reinterpret_cast<uint4 *>(B.digests + i * 32u);
-            auto bswap = [](uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); };
-            out[0] = make_uint4(bswap(h[0]), bswap(h[1]), bswap(h[2]), bswap(h[3]));
-            out[1] = make_uint4(bswap(h[4]), bswap(h[5]), bswap(h[6]), bswap(h[7]));
         }
     }
 }
+
+// Byte histograms, one wave per chunk (a wave takes chunks w, w + waves, ...):
+// the frequency count of entropy() (snapshot/backup.go:548-557).  Unlike the
+// SHA-256 chain a histogram has no order, so the wave reads its chunk
+// coalesced, 16 bytes per lane per step, and counts into 8 LDS copies of the
+// 256 bins (copy = lane & 7, bin b of copy c at dword 8 b + c: lanes of one
+// copy only collide on equal bytes); then the copies are summed, one uint4
+// of bins per lane, into the chunk's row.
+constexpr uint32_t kHistWaves = 4, kHistCopies = 8;
+
+__global__ __launch_bounds__(kHistWaves * 64) void k_chunk_hist(const DigestBatch DB)
+{
+    __shared__ uint32_t s_h[kHistWaves][256 * kHistCopies];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const DigestBuf &B = DB.b[blockIdx.y];
+    if (!B.hist) return;
+    uint32_t *h = s_h[wave];
+    const uint32_t cpy = lane & (kHistCopies - 1u);
+    const uint64_t n_cuts = chunk_count(B);
+    const uint64_t waves = uint64_t(gridDim.x) * kHistWaves;
+    for (uint64_t c = uint64_t(blockIdx.x) * kHistWaves + wave; c < n_cuts; c += waves) {
+#pragma unroll
+        for (uint32_t i = 0; i < 256 * kHistCopies / 64; ++i) h[i * 64 + lane] = 0;
+        uint64_t off, n;
+        cut_at(B, c, off, n);
+        const uint8_t *p = B.data + off;
+        // 16-B aligned steps covering [p, p + n); bytes outside it are skipped
+        const uint64_t a0 = reinterpret_cast<uintptr_t>(p) & ~15ull, end = reinterpret_cast<uintptr_t>(p) + n;
+        auto count = [&](uint32_t byte) {
+            __hip_atomic_fetch_add(h + byte * kHistCopies + cpy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        for (uint64_t a = a0 + 16u * lane; n && a < end; a += 1024u) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(uintptr_t(a));
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+            if (a >= reinterpret_cast<uintptr_t>(p) && a + 16u <= end) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    count(wd[q] & 0xFFu);
+                    count(__builtin_amdgcn_ubfe(wd[q], 8, 8));
+                    count(__builtin_amdgcn_ubfe(wd[q], 16, 8));
+                    count(wd[q] >> 24);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint64_t x = a + uint64_t(q);
+                    if (x >= reinterpret_cast<uintptr_t>(p) && x < end) count((wd[q >> 2] >> (8 * (q & 3))) & 0xFFu);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        uint32_t sum[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+#pragma unroll
+            for (uint32_t k = 0; k < kHistCopies; ++k) sum[j] += h[(4 * lane + j) * kHistCopies + k];
+        reinterpret_cast<uint4 *>(B.hist + c * 256u)[lane] = make_uint4(sum[0], sum[1], sum[2], sum[3]);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+uint64_t g_digest_lanes = 0;  // cdc_debug_set_digest_lanes (0: from the device's CU count)
 
 int launch_digests(const DigestBatch &DB, void *stream)
 {
@@ -265,12 +420,24 @@ int launch_digests(const DigestBatch &DB, void *stream)
         hist |= DB.b[i].hist != nullptr;
     }
     if (cap == 0 || DB.nbufs == 0) return CDC_OK;
-    if ((cap + 63) / 64 > 0x7FFFFFFFull) return CDC_E_INVALID;
-    const dim3 grid(uint32_t((cap + 63) / 64), DB.nbufs), block(hist ? 192 : 128);
-    if (hist)
-        hipLaunchKernelGGL(k_chunk_digest<true>, grid, block, kRingBytes + kHistPairBytes, st, DB);
-    else
-        hipLaunchKernelGGL(k_chunk_digest<false>, grid, block, kRingBytes, st, DB);
+    if (cap > 0xFFFFFFFFull) return CDC_E_INVALID;  // chunk indices relative to a workgroup's first are u32
+    static const uint32_t cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return uint32_t(n);
+    }();
+    // two SHA-256 workgroups per CU (~66 KiB of LDS each)
+    DigestBatch D = DB;
+    D.resident_lanes = g_digest_lanes ? g_digest_lanes : uint64_t(cus) * (4u / kDigestGroups) * 64u * kDigestGroups;
+    const uint32_t lanes_per_wg = 64u * kDigestGroups;
+    hipLaunchKernelGGL(k_chunk_digest, dim3(uint32_t((cap + lanes_per_wg - 1) / lanes_per_wg), DB.nbufs),
+                       dim3(kDigestWaves * 64), 0, st, D);
+    if (hist) {  // a wave per chunk; up to 8 workgroups per CU
+        const uint64_t wgs = std::min<uint64_t>((cap + kHistWaves - 1) / kHistWaves, uint64_t(cus) * 8u);
+        hipLaunchKernelGGL(k_chunk_hist, dim3(uint32_t(wgs), DB.nbufs), dim3(kHistWaves * 64), 0, st, D);
+    }
     return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
 }
 

@@ -116,8 +116,10 @@ struct DigestBuf {
 };
 struct DigestBatch {
     uint32_t nbufs;
+    uint64_t resident_lanes;  // lanes the device keeps resident at once (set by launch_digests)
     DigestBuf b[kMaxBufsPerLaunch];
 };
 int launch_digests(const DigestBatch &DB, void *stream);
+extern uint64_t g_digest_lanes;
 
 }  // namespace cdc

@@ -221,6 +221,47 @@ def test_gpu_digest_batch_many_buffers():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 3, 64, 100])
+def test_gpu_digest_multi_chunk_lanes(lanes):
+    """A launch with more chunks than resident lanes gives each lane a run of
+    consecutive chunks (k = ceil(chunks / lanes)): forced here with small lane
+    counts over the padding-boundary lengths at every alignment, empty chunks,
+    gaps and overlaps, chunks past 1023 blocks (histogram halves flushed
+    mid-chunk and accumulated), and several buffers in one launch group."""
+    torch = _gpu()
+    from plakar_amd import _lib, hashing
+    _lib.ensure_init()
+    L = _lib.lib()
+    buf = random_bytes(3 << 20, 13)
+    lens = [0, 1, 55, 56, 63, 64, 65, 119, 120, 4095, 65537, 0, 70000, 200000, 3, 127]
+    cuts, o = [], 0
+    for k, n in enumerate(lens * 3):
+        o += k % 5
+        cuts.append((o, n))
+        o += n
+    cuts.append((100, 5000))  # overlaps an earlier chunk
+    assert o < buf.size
+    refs = [(buf, cuts)]
+    for k in range(3):  # more buffers in the same launch group, counts bounded by result rows
+        b2 = random_bytes(300000 + 977 * k, 50 + k)
+        c2 = [(i * 997 % 1000, 1000 + (i * 7919) % 30000) for i in range(40)]
+        refs.append((b2, c2))
+    try:
+        assert L.cdc_debug_set_digest_lanes(lanes) == 0
+        bufs = [torch.from_numpy(np.ascontiguousarray(b)).cuda() for b, _ in refs]
+        cls = [torch.tensor(np.asarray(c, np.int64).reshape(-1, 2), device="cuda") for _, c in refs]
+        res = [torch.tensor([len(c) - (i % 2), 0, 0, 0], dtype=torch.int64, device="cuda")
+               for i, (_, c) in enumerate(refs)]
+        outs = hashing.chunk_digests_batch(bufs, cls, res)
+        torch.cuda.synchronize()
+    finally:
+        L.cdc_debug_set_digest_lanes(0)
+    for i, ((b, c), (d, h)) in enumerate(zip(refs, outs)):
+        keep = len(c) - (i % 2)
+        _check(b, c[:keep], d[:keep].cpu().numpy(), h[:keep].cpu().numpy())
+
+
+@pytest.mark.gpu
 def test_gpu_chunkify_batch_objects(oracle):
     """snapshot.chunkify_batch against the reference's per-file work restated
     on the CPU: routing (backup.go:631-645), oracle cuts, hashlib chunk and
