@@ -155,8 +155,9 @@ def digest_leg(torch, batch, bufs, reps, check):
     longest = max(int(c[:, 1].max().item()) for c in cuts if c.shape[0])
     nchunks = sum(int(c.shape[0]) for c in cuts)
     d = dict(value=round(total / (ms * 1e-3) / GIB, 2), unit="GiB/s", ms_per_pass=round(ms, 3), chunks=nchunks,
-             longest_chunk=longest, kernel="k_chunk_digest (SHA-256 + 256-bin histogram; per chunk a producer lane and a round lane)",
-             bound="the round lane's serial chain: the longest chunk's 64-B blocks x ~905 VALU at one wave per SIMD")
+             longest_chunk=longest, kernel="k_chunk_digest (SHA-256: per chunk a producer lane and a round lane) + k_chunk_hist (a wave per chunk)",
+             bound="one launch lasts as long as its longest chunk's SHA-256 chain: 64-B blocks x ~905 VALU of one "
+                   "round wave per block")
     if check:
         host = bufs[0][:min(bufs[0].numel(), 256 << 20)].cpu().numpy()
         c0 = cuts[0].cpu().numpy()
