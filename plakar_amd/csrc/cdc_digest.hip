@@ -174,8 +174,11 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
         // the slot it consumes.
         const uint32_t *dummy = reinterpret_cast<const uint32_t *>(B.cuts);
         uint64_t lc = C0 + 64u * grp + lane, loff = 0, ln = 0, lnb = 0, lb = 0;  // load cursor
-        bool lhas = lc < C1;
-        if (lhas) {
+        // load-cursor flags in ONE variable: two bools captured by reference got a
+        // pointer select and went to scratch, with a vmcnt(0) on every block
+        constexpr uint32_t kHas = 1u, kResv = 2u;  // the cursor has a chunk; its next one is requested
+        uint32_t lst = lc < C1 ? kHas : 0u;
+        if (lst & kHas) {
             cut_at(B, lc, loff, ln);
             lnb = sha_blocks(ln);
         }
@@ -185,32 +188,30 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
         // a lane does not hold a chunk it will only start much later (the
         // launch's tail), early enough to hide the cut's load
         uint64_t cn = ~0ull, noff = 0, nn = 0;
-        bool resv = false;
-        auto reserve = [&]() {
+        auto reserve = [&]() __attribute__((always_inline)) {
             cn = C0 + __hip_atomic_fetch_add(&s_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (cn < C1) cut_at(B, cn, noff, nn);
             else cn = ~0ull;
-            resv = true;
+            lst |= kResv;
         };
         struct Blk {
             uint32_t x[17];  // q[16 b .. 16 b + 16]
-            uint32_t sel, crel, n, itc;
-            bool live;
+            uint32_t sel, crel, n, itc;  // crel = kNoChunk: the lane has no block
         };
-        auto issue = [&](Blk &k) {  // the load cursor's block into k, then advance the cursor
-            const bool real = lhas && ln != 0;
+        constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
+        auto issue = [&](Blk &k) __attribute__((always_inline)) {  // the load cursor's block into k, then advance the cursor
+            const bool real = (lst & kHas) && ln != 0;
             const uint32_t *q = real ? LA.q : dummy;
             const uint64_t base = real ? 16u * lb : 0u, lim = real ? LA.lastq : 0u;
 #pragma unroll
             for (int j = 0; j < 17; ++j) k.x[j] = q[min<uint64_t>(base + j, lim)];
-            k.live = lhas;
             k.sel = LA.sel;
-            k.crel = uint32_t(lc - C0);
+            k.crel = (lst & kHas) ? uint32_t(lc - C0) : kNoChunk;
             k.n = uint32_t(ln);
             k.itc = uint32_t(lb);
-            if (lhas) {
+            if (lst & kHas) {
                 ++lb;
-                if (!resv && lb + 1u >= lnb) reserve();
+                if (!(lst & kResv) && lb + 1u >= lnb) reserve();
                 if (lb == lnb) {
                     if (cn != ~0ull) {
                         lc = cn;
@@ -219,16 +220,16 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
                         lnb = sha_blocks(nn);
                         lb = 0;
                         LA = chunk_words(B.data, loff, ln);
-                        resv = false;
+                        lst = kHas;
                     } else {
-                        lhas = false;
+                        lst = 0u;
                     }
                 }
             }
         };
         // schedule block `it` from slot k; false once no lane of the workgroup has one
-        auto step = [&](uint32_t it, const Blk &k) -> bool {
-            const bool live = k.live;
+        auto step = [&](uint32_t it, const Blk &k) __attribute__((always_inline)) -> bool {
+            const bool live = k.crel != kNoChunk;
             const bool last = live && k.itc + 1u == sha_blocks(k.n);  // the chunk's final block
             uint32_t w[16];
 #pragma unroll
