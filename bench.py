@@ -40,8 +40,8 @@ WORKLOADS = {
                     "share), host buffers in -> cut lists in host memory (PCIe-inclusive)",
                nbuf=512, size=0, kind="zipf", host=True),
     "c4f": dict(desc="C4 from files: the same 512-file share written to disk once (untimed), then per step read by the "
-                     "library (pread, 16 threads) into its pinned arena and chunked (pinned H2D, cut lists to host); "
-                     "warm page cache",
+                     "library (pread, 16 threads) into its pinned arena and chunked (pinned H2D, cut lists to host), "
+                     "the reads running ahead of the device by 256-MiB sub-batches; warm page cache",
                 nbuf=512, size=0, kind="zipf", host=True, files=True),
 }
 
@@ -480,8 +480,7 @@ def main():
 
             def step():
                 fbatch.reset()
-                fbatch.add_files(paths, threads=16)
-                return fbatch.chunk(opts)
+                return fbatch.add_and_chunk(paths, opts, threads=16)
     else:
         size = (args.size_mib << 20) if args.size_mib else wl["size"]
         bufs = make_buffers(torch, wl, rank, dev, size, world)

@@ -207,6 +207,7 @@ void cdc_packer_free(cdc_packer *p);
  *   cdc_batch_reserve    append a buffer of len bytes; *ptr = where to write it
  *   cdc_batch_add_fd     append len bytes read from fd (pread from offset 0)
  *   cdc_batch_add_files  append n whole files, read by `threads` threads;
+ *   cdc_batch_chunk_files  add_files + chunking of those files, overlapped;
  *                        sizes[i] = file sizes (may be NULL).  All or nothing.
  *   cdc_batch_chunk      cdc_chunk over the arena's buffers, in order
  * Errors: CDC_E_NOSPACE (arena full), CDC_E_IO, CDC_E_NOT_INIT. */
@@ -215,6 +216,13 @@ int cdc_batch_new(uint64_t capacity, cdc_batch **out);
 int cdc_batch_reserve(cdc_batch *b, uint64_t len, uint8_t **ptr);
 int cdc_batch_add_fd(cdc_batch *b, int fd, uint64_t len);
 int cdc_batch_add_files(cdc_batch *b, const char *const *paths, int n, int threads, uint64_t *sizes);
+/* cdc_batch_add_files + cdc_chunk over the n files it adds (not the arena's
+ * earlier buffers), overlapped: reader threads run ahead while each
+ * sub-batch of >= 256 MiB of whole files is chunked as soon as it is read.
+ * out / out_counts (n entries) / out_needed as cdc_chunk. */
+int cdc_batch_chunk_files(cdc_batch *b, const char *const *paths, int n, int threads, const cdc_opts *opts,
+                          cdc_cut *out, uint64_t out_cap, uint64_t *out_counts, uint64_t *out_needed,
+                          uint64_t *sizes);
 int cdc_batch_count(const cdc_batch *b);
 int cdc_batch_get(const cdc_batch *b, int i, const uint8_t **ptr, uint64_t *len);
 int cdc_batch_chunk(cdc_batch *b, const cdc_opts *opts, cdc_cut *out, uint64_t out_cap,

@@ -108,6 +108,9 @@ SIGNATURES = {
                                            _P(ctypes.c_uint64)]),
     "cdc_batch_count": (ctypes.c_int, [ctypes.c_void_p]),
     "cdc_batch_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _P(_P(ctypes.c_uint8)), _P(ctypes.c_uint64)]),
+    "cdc_batch_chunk_files": (ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_char_p), ctypes.c_int, ctypes.c_int,
+                                             _P(cdc_opts), _P(cdc_cut), ctypes.c_uint64, _P(ctypes.c_uint64),
+                                             _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
     "cdc_batch_chunk": (ctypes.c_int, [ctypes.c_void_p, _P(cdc_opts), _P(cdc_cut), ctypes.c_uint64,
                                        _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
     "cdc_batch_reset": (None, [ctypes.c_void_p]),

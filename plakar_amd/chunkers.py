@@ -201,6 +201,33 @@ class FileBatch:
         check(lib().cdc_batch_add_files(self._h, arr, n, int(threads), sizes), "cdc_batch_add_files")
         return [int(sizes[i]) for i in range(n)]
 
+    def add_and_chunk(self, paths, opts, threads=8):
+        """add_files(paths) and the chunking of those files, overlapped
+        (cdc_batch_chunk_files: reader threads run ahead of the device, which
+        chunks each >= 256-MiB sub-batch of whole files once it is read).
+        Returns per file a uint64 (n, 2) array of (offset, length) rows."""
+        import numpy as np
+        o = opts._c()
+        check(lib().cdc_validate(b"fastcdc", ctypes.byref(o)), "FileBatch.add_and_chunk")
+        n = len(paths)
+        arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        sizes = (ctypes.c_uint64 * max(n, 1))()
+        cap = sum(os.path.getsize(p) // max(opts.MinSize, 1) + 2 for p in paths)
+        out = np.zeros((max(cap, 1), 2), dtype=np.uint64)
+        counts = (ctypes.c_uint64 * max(n, 1))()
+        needed = ctypes.c_uint64()
+        check(lib().cdc_batch_chunk_files(self._h, arr, n, int(threads), ctypes.byref(o),
+                                          ctypes.cast(out.ctypes.data, ctypes.POINTER(_lib.cdc_cut)), out.shape[0],
+                                          counts, ctypes.byref(needed), sizes), "FileBatch.add_and_chunk")
+        res, k = [], 0
+        for i in range(n):
+            c = counts[i]
+            part = out[k:k + c].copy()
+            part[:, 1] &= np.uint64(0xFFFFFFFF)
+            res.append(part)
+            k += c
+        return res
+
     def add_fd(self, fd, length):
         check(lib().cdc_batch_add_fd(self._h, int(fd), int(length)), "cdc_batch_add_fd")
 

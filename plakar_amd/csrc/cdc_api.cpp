@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1043,6 +1044,102 @@ extern "C" int cdc_batch_add_files(cdc_batch *b, const char *const *paths, int n
         fd = -1;
     }
     return CDC_OK;
+}
+
+// cdc_batch_add_files + chunking of the added files, overlapped: the files
+// are split into consecutive sub-batches of >= kSubBatchBytes; reader threads
+// run ahead through the files in order while this thread chunks each
+// sub-batch (pinned H2D + kernels, cdc_chunk) as soon as all of its files are
+// in the arena.
+static constexpr uint64_t kSubBatchBytes = 256ull << 20;
+
+extern "C" int cdc_batch_chunk_files(cdc_batch *b, const char *const *paths, int n, int threads, const cdc_opts *opts,
+                                     cdc_cut *out, uint64_t out_cap, uint64_t *out_counts, uint64_t *out_needed,
+                                     uint64_t *sizes)
+{
+    if (!b || n < 0 || (n > 0 && (!paths || !out_counts)) || !opts) return CDC_E_INVALID;
+    const int v = validate_sizes(opts);
+    if (v != CDC_OK) return v;
+    if (!G().init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
+    const size_t first = b->bufs.size();
+    const uint64_t used0 = b->used;
+    std::vector<int> fds(size_t(n), -1);
+    auto undo = [&](int st) {
+        for (int fd : fds)
+            if (fd >= 0) close(fd);
+        b->bufs.resize(first);
+        b->used = used0;
+        return st;
+    };
+    std::vector<int> sub_end;  // file index one past each sub-batch
+    uint64_t acc = 0;
+    for (int i = 0; i < n; ++i) {
+        struct stat sb;
+        fds[size_t(i)] = open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fds[size_t(i)] < 0 || fstat(fds[size_t(i)], &sb) != 0) return undo(CDC_E_IO);
+        uint8_t *p = nullptr;
+        const int st = cdc_batch_reserve(b, uint64_t(sb.st_size), &p);
+        if (st != CDC_OK) return undo(st);
+        if (sizes) sizes[i] = uint64_t(sb.st_size);
+        acc += uint64_t(sb.st_size);
+        if (acc >= kSubBatchBytes || i + 1 == n) {
+            sub_end.push_back(i + 1);
+            acc = 0;
+        }
+    }
+    std::vector<int> sub_of(static_cast<size_t>(n));
+    for (size_t j = 0, i = 0; j < sub_end.size(); ++j)
+        for (; int(i) < sub_end[j]; ++i) sub_of[i] = int(j);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int> left(sub_end.size());  // files of each sub-batch still being read
+    for (size_t j = 0; j < sub_end.size(); ++j) left[j] = sub_end[j] - (j ? sub_end[j - 1] : 0);
+    std::atomic<int> next{0}, err{CDC_OK};
+    auto work = [&] {
+        for (int i; (i = next.fetch_add(1)) < n && err.load() == CDC_OK;) {
+            const cdc_buf &cb = b->bufs[first + size_t(i)];
+            const int st = read_full(fds[size_t(i)], static_cast<uint8_t *>(const_cast<void *>(cb.data)), cb.len);
+            if (st != CDC_OK) err.store(st);
+            std::lock_guard<std::mutex> lk(mu);
+            --left[size_t(sub_of[size_t(i)])];
+            cv.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        cv.notify_all();
+    };
+    const int nt = std::max(1, std::min(threads, n));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t) pool.emplace_back(work);
+    int status = CDC_OK;
+    uint64_t k = 0, needed = 0;
+    for (size_t j = 0; j < sub_end.size() && status != CDC_E_IO; ++j) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return left[j] == 0 || err.load() != CDC_OK; });
+        }
+        if (err.load() != CDC_OK) break;
+        const int s0 = j ? sub_end[j - 1] : 0, cnt = sub_end[j] - s0;
+        uint64_t need = 0;
+        const bool room = status == CDC_OK;
+        const int st = cdc_chunk(b->bufs.data() + first + size_t(s0), cnt, opts, room ? out + k : nullptr,
+                                 room ? out_cap - k : 0, out_counts + s0, &need);
+        needed += need;
+        if (st == CDC_OK) k += need;
+        else if (st == CDC_E_NOSPACE) status = CDC_E_NOSPACE;  // keep counting what is needed
+        else {
+            status = st;
+            break;
+        }
+    }
+    if (status != CDC_OK && status != CDC_E_NOSPACE) err.store(status);  // readers stop early
+    for (auto &t : pool) t.join();
+    if (err.load() != CDC_OK) return undo(err.load());
+    for (int &fd : fds) {
+        close(fd);
+        fd = -1;
+    }
+    if (out_needed) *out_needed = needed;
+    return status;
 }
 
 extern "C" int cdc_batch_count(const cdc_batch *b) { return b ? int(b->bufs.size()) : 0; }

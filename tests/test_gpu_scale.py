@@ -152,6 +152,43 @@ def test_file_batch_pinned_arena(oracle, tmp_path):
     fb.close()
 
 
+def test_file_batch_chunk_files_overlapped(oracle, tmp_path):
+    """cdc_batch_chunk_files: the files read into the arena by reader threads
+    while the device chunks each >= 256-MiB sub-batch (here two) as soon as
+    it is read; cut lists vs the oracle, bytes kept in the arena, and
+    CDC_E_NOSPACE with the needed count when the cut array is short."""
+    import ctypes
+    _lib.ensure_init()
+    sizes = [0, 1, 65535, 150 << 20, 3 << 20, 130 << 20, 77_000, 40 << 20]
+    paths, datas = [], []
+    for i, n in enumerate(sizes):
+        a = random_bytes(n, 800 + i)
+        p = tmp_path / f"g{i}"
+        p.write_bytes(a.tobytes())
+        paths.append(str(p))
+        datas.append(a)
+    cap = sum((n + 4095) // 4096 * 4096 for n in sizes)
+    fb = chunkers.FileBatch(cap)
+    res = fb.add_and_chunk(paths, OPTS, threads=8)
+    assert len(fb) == len(sizes)
+    gear = _lib.default_gear()
+    for i, a in enumerate(datas):
+        assert np.array_equal(fb.buffer(i), a)
+        assert_same(res[i], oracle.chunk(a, gear, **DEF), f"file {i}")
+    total = sum(r.shape[0] for r in res)
+    fb.reset()
+    L = _lib.lib()
+    n = len(paths)
+    arr = (ctypes.c_char_p * n)(*[p.encode() for p in paths])
+    out = (_lib.cdc_cut * 3)()
+    counts = (ctypes.c_uint64 * n)()
+    needed = ctypes.c_uint64()
+    st = L.cdc_batch_chunk_files(fb._h, arr, n, 4, ctypes.byref(OPTS._c()), out, 3, counts, ctypes.byref(needed), None)
+    assert st == _lib.CDC_E_NOSPACE and needed.value == total
+    assert [counts[i] for i in range(n)] == [r.shape[0] for r in res]
+    fb.close()
+
+
 def test_backup_batch_packfiles(oracle):
     """chunkify on the device -> PutBlob of every new chunk -> packfiles (the
     re-plumbed snapshot/backup.go:594-629 + snapshot/packer.go): each packfile
