@@ -554,7 +554,7 @@ def main():
     digest = None
     if not host_mode and args.digest_reps > 0:
         digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0 and world == 1)
-        digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_window, 4)
+        digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_window, 8)
 
     encode_res = None
     if not host_mode and args.encode_reps > 0:
