@@ -70,6 +70,13 @@ def main():
     print(f"\ntimed region on the device: {span:.1f} us for {a.steps} passes = {span / a.steps:.4f} ms/pass")
     for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         print(f"  {k:16s} n={len(v):4d} avg={sum(v) / len(v):8.2f} min={min(v):8.2f} max={max(v):8.2f}")
+    # bench.py's roofline loop: the next max(5, min(K, 50)) passes, one stream,
+    # the scan alone on the device (its roofline.kernel_avg_ms)
+    rsteps = max(5, min(a.steps, 50))
+    roof = [(ks[i][1] - ks[i][0]) / 1e3 for i in starts[npass:npass + rsteps]]
+    if len(roof) == rsteps:
+        print(f"\nroofline loop (passes {npass}-{npass + rsteps - 1}, one stream): scan avg {sum(roof) / len(roof):.2f} us "
+              f"min {min(roof):.2f} max {max(roof):.2f}")
 
 
 if __name__ == "__main__":
