@@ -1373,6 +1373,8 @@ struct WsCache {
     std::mutex mu;
     uint8_t *p = nullptr;
     size_t cap = 0;
+    uint8_t *hp = nullptr;  // pinned staging of the host plan (one DMA instead of pageable copies)
+    size_t hcap = 0;
     hipStream_t aux = nullptr;  // k_xxh32 runs here, beside the LZ4 and GCM kernels
     hipEvent_t fork = nullptr, join = nullptr;
 };
@@ -1490,16 +1492,32 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     Bt.xx_ids = reinterpret_cast<uint32_t *>(ws + o_xx);
     const uint32_t xx_wgs = (n + kXxWaves * kXxPerWave - 1) / (kXxWaves * kXxPerWave);
     bool ok = true;
-    auto h2d = [&](size_t o, const void *p, size_t bytes) {
-        if (bytes) ok = ok && hipMemcpyAsync(ws + o, p, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+    // The plan's tables at their workspace offsets [0, o_key + 32) in pinned
+    // staging, XXH32 order after them: two DMAs.  (The call ends with a
+    // stream sync under C.mu, so the staging is free again on return.)
+    const size_t h_prefix = o_key + 32, h_xx = align16(h_prefix), h_need = h_xx + (compress ? nb * 4 : 0);
+    if (C.hcap < h_need) {
+        if (C.hp) (void)hipHostFree(C.hp);
+        C.hp = nullptr;
+        C.hcap = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&C.hp), h_need, hipHostMallocDefault) != hipSuccess)
+            return CDC_E_NOMEM;
+        C.hcap = h_need;
+    }
+    auto stage = [&](size_t o, const void *p, size_t bytes) {
+        if (bytes) std::memcpy(C.hp + o, p, bytes);
     };
-    h2d(o_blobs, blobs.data(), nb * sizeof(BlobDesc));
-    h2d(o_blks, blks.data(), nk * sizeof(Blk));
-    h2d(o_segs, segs.data(), ng * sizeof(Seg));
-    if (compress) h2d(o_xx, xx_ids.data(), nb * 4);
+    stage(o_blobs, blobs.data(), nb * sizeof(BlobDesc));
+    stage(o_blks, blks.data(), nk * sizeof(Blk));
+    stage(o_segs, segs.data(), ng * sizeof(Seg));
     if (encrypt) {
-        h2d(o_rnd, random, nb * 56);
-        h2d(o_key, key, 32);
+        stage(o_rnd, random, nb * 56);
+        stage(o_key, key, 32);
+    }
+    ok = hipMemcpyAsync(ws, C.hp, h_prefix, hipMemcpyHostToDevice, s) == hipSuccess;
+    if (compress && nb) {
+        stage(h_xx, xx_ids.data(), nb * 4);
+        ok = ok && hipMemcpyAsync(ws + o_xx, C.hp + h_xx, nb * 4, hipMemcpyHostToDevice, s) == hipSuccess;
     }
     if (ok && n) {
         if (compress) {
