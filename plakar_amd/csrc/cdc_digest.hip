@@ -428,7 +428,7 @@ int launch_digests(const DigestBatch &DB, void *stream)
     }();
     // two SHA-256 workgroups per CU (~66 KiB of LDS each)
     DigestBatch D = DB;
-    D.resident_lanes = g_digest_lanes ? g_digest_lanes : uint64_t(cus) * (4u / kDigestGroups) * 64u * kDigestGroups;
+    D.resident_lanes = g_digest_lanes ? g_digest_lanes : uint64_t(cus) * 2u * 64u * kDigestGroups;
     const uint32_t lanes_per_wg = 64u * kDigestGroups;
     hipLaunchKernelGGL(k_chunk_digest, dim3(uint32_t((cap + lanes_per_wg - 1) / lanes_per_wg), DB.nbufs),
                        dim3(kDigestWaves * 64), 0, st, D);
