@@ -135,6 +135,7 @@ constexpr uint32_t kDigestWaves = 2 * kDigestGroups;
 // read by the rounds one block behind): the chunk (relative to the
 // workgroup's first) and flags.
 constexpr uint32_t kMetaLive = 1u << 9, kMetaLast = 1u << 10;  // bits 0-8: rb + 128
+constexpr uint32_t kSortCap = 1024;  // chunks a workgroup sorts longest first (8 KiB of LDS)
 
 __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const DigestBatch DB)
 {
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
     __shared__ uint32_t s_meta[kDigestGroups][kShaRing][2][64];
     __shared__ uint32_t s_any[kShaRing][kDigestGroups];  // some lane of the group holds a block in that stage
     __shared__ uint32_t s_next;                          // the workgroup's chunk queue (relative)
+    __shared__ uint64_t s_order[kSortCap];               // its chunks longest first: (length << 32) | index
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t grp = wave % kDigestGroups;
     const uint32_t role = wave / kDigestGroups;  // 0 producer, 1 rounds
@@ -163,7 +165,38 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
     if (C0 >= n_cuts) return;  // whole workgroup: no barrier is left waiting
     const uint64_t C1 = min(C0 + kLanes * k, n_cuts);
     if (threadIdx.x == 0) s_next = kLanes;
+    // With more chunks than lanes, the queue hands them out longest first
+    // (LPT: the short ones fill the lanes' ends), sorted in LDS by a bitonic
+    // network when they fit kSortCap.
+    const uint32_t nq = uint32_t(C1 - C0);
+    const bool sorted = nq > kLanes && nq <= kSortCap;
+    if (sorted) {
+        uint32_t m = kLanes;
+        while (m < nq) m <<= 1;
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            uint64_t o = 0, len = 0;
+            if (i < nq) cut_at(B, C0 + i, o, len);
+            s_order[i] = i < nq ? (len << 32) | i : 0ull;  // padding sorts last
+        }
+        __syncthreads();
+        for (uint32_t size = 2; size <= m; size <<= 1) {
+            for (uint32_t stride = size >> 1; stride; stride >>= 1) {
+                for (uint32_t t = threadIdx.x; t < m / 2; t += blockDim.x) {
+                    const uint32_t i = 2 * stride * (t / stride) + t % stride, j = i + stride;
+                    const bool desc = (i & size) == 0;  // descending runs, merged into one descending order
+                    const uint64_t a = s_order[i], b = s_order[j];
+                    if ((a < b) == desc) {
+                        s_order[i] = b;
+                        s_order[j] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
     __syncthreads();
+    // the workgroup's q-th chunk in queue order
+    auto queued = [&](uint32_t q) -> uint64_t { return C0 + (sorted ? uint32_t(s_order[q]) : q); };
 
     if (role == 0) {
         // Blocks are loaded two ahead of the one being scheduled (a lane's
@@ -173,7 +206,8 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
         // block reads the cut list), so the compiler's vmcnt waits only for
         // the slot it consumes.
         const uint32_t *dummy = reinterpret_cast<const uint32_t *>(B.cuts);
-        uint64_t lc = C0 + 64u * grp + lane, loff = 0, ln = 0, lnb = 0, lb = 0;  // load cursor
+        const uint32_t q0 = 64u * grp + lane;
+        uint64_t lc = q0 < nq ? queued(q0) : C1, loff = 0, ln = 0, lnb = 0, lb = 0;  // load cursor
         // load-cursor flags in ONE variable: two bools captured by reference got a
         // pointer select and went to scratch, with a vmcnt(0) on every block
         constexpr uint32_t kHas = 1u, kResv = 2u;  // the cursor has a chunk; its next one is requested
@@ -189,9 +223,9 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
         // launch's tail), early enough to hide the cut's load
         uint64_t cn = ~0ull, noff = 0, nn = 0;
         auto reserve = [&]() __attribute__((always_inline)) {
-            cn = C0 + __hip_atomic_fetch_add(&s_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (cn < C1) cut_at(B, cn, noff, nn);
-            else cn = ~0ull;
+            const uint32_t q = __hip_atomic_fetch_add(&s_next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            cn = q < nq ? queued(q) : ~0ull;
+            if (cn != ~0ull) cut_at(B, cn, noff, nn);
             lst |= kResv;
         };
         struct Blk {

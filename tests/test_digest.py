@@ -262,6 +262,36 @@ def test_gpu_digest_multi_chunk_lanes(lanes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 128, 700])
+def test_gpu_digest_queue_order(lanes):
+    """Workgroups with more chunks than lanes: up to 1,024 of them handed out
+    longest first (a bitonic sort in LDS), more in cut-list order; lengths
+    spread from 0 to 40 KiB so that the order matters."""
+    torch = _gpu()
+    from plakar_amd import _lib, hashing
+    _lib.ensure_init()
+    L = _lib.lib()
+    buf = random_bytes(24 << 20, 17)
+    rng = np.random.default_rng(5)
+    cuts, o = [], 0
+    while True:
+        n = int(rng.integers(0, 40000)) if rng.random() < 0.9 else 0
+        if o + n > buf.size or len(cuts) >= 1500:
+            break
+        cuts.append((o, n))
+        o += n
+    try:
+        assert L.cdc_debug_set_digest_lanes(lanes) == 0
+        t = torch.from_numpy(buf).cuda()
+        c = torch.tensor(np.asarray(cuts, np.int64), device="cuda")
+        d, h = hashing.chunk_digests(t, c)
+        torch.cuda.synchronize()
+    finally:
+        L.cdc_debug_set_digest_lanes(0)
+    _check(buf, cuts, d.cpu().numpy(), h.cpu().numpy())
+
+
+@pytest.mark.gpu
 def test_gpu_chunkify_batch_objects(oracle):
     """snapshot.chunkify_batch against the reference's per-file work restated
     on the CPU: routing (backup.go:631-645), oracle cuts, hashlib chunk and
