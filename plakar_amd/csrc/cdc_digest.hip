@@ -409,8 +409,20 @@ __global__ __launch_bounds__(kHistWaves * 64) void k_chunk_hist(const DigestBatc
         auto count = [&](uint32_t byte) {
             __hip_atomic_fetch_add(h + byte * kHistCopies + cpy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         };
+        // the next step's 16 bytes in flight while this step counts; every
+        // lane loads every step (from a block holding chunk bytes: the last
+        // one when past the end), so the compiler waits only for the current
+        const uint64_t alast = (end - 1) & ~15ull;
+        auto ld = [&](uint64_t a) {  // global (not flat) loads: LDS waits do not wait for them
+            typedef __attribute__((address_space(1))) const uint64_t g64;
+            const g64 *q = reinterpret_cast<const g64 *>(uintptr_t(a <= alast ? a : alast));
+            const uint64_t x = q[0], y = q[1];
+            return make_uint4(uint32_t(x), uint32_t(x >> 32), uint32_t(y), uint32_t(y >> 32));
+        };
+        uint4 vn = n ? ld(a0 + 16u * lane) : make_uint4(0, 0, 0, 0);
         for (uint64_t a = a0 + 16u * lane; n && a < end; a += 1024u) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(uintptr_t(a));
+            const uint4 v = vn;
+            vn = ld(a + 1024u);
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
             if (a >= reinterpret_cast<uintptr_t>(p) && a + 16u <= end) {
 #pragma unroll
