@@ -386,6 +386,72 @@ def cpu_threads_leg(orc, gear, kw, bufs_host, threads, seconds):
                        f"in {el:.1f} s, {threads} threads")
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(argv, n):
+    """`python bench.py --gpus N` with no launcher: start N rank processes of
+    this script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous
+    on 127.0.0.1), wait for all of them and return the worst exit status.  The
+    parent never initialises HIP (device_count() does not, on this image); it
+    refuses to run when fewer than N devices are visible (unless every rank is
+    told to share device 0: BENCH_REHEARSE_ONE_GPU=1, or BENCH_CPU_SELFTEST=1)."""
+    import subprocess
+    shared = os.environ.get("BENCH_REHEARSE_ONE_GPU") == "1" or os.environ.get("BENCH_CPU_SELFTEST") == "1"
+    if not shared:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} device(s) visible", file=sys.stderr)
+            return 2
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                              env=dict(base, RANK=str(i), LOCAL_RANK=str(i))) for i in range(n)]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def gather_per_rank(dist, world, value, dev):
+    """Every rank's host float, in rank order (rank 0 reports each rank's rate)."""
+    if world == 1:
+        return [value]
+    import torch
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=on)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
+def cpu_selftest(args, world, rank):
+    """BENCH_CPU_SELFTEST=1: the multi-rank plumbing alone (rendezvous, barrier,
+    max-over-ranks time, per-rank gather, the JSON line) over gloo, no GPU.
+    Each rank "chunks" by sleeping; tests/test_dist.py runs it without a
+    launcher to check that --gpus N starts N ranks."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (1 + rank))
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = reduce_max(dist, world, el, None)
+    per = gather_per_rank(dist, world, el, None)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "selftest": True,
+                          "elapsed_max_s": elapsed, "per_rank_elapsed_s": per}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -418,11 +484,16 @@ def main():
     if args.warmup is None:
         args.warmup = 2 if host_default else 200
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))  # before anything touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("BENCH_CPU_SELFTEST") == "1":
+        return cpu_selftest(args, world, rank)
 
     import torch
     import torch.distributed as dist
@@ -508,6 +579,7 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = reduce_max(dist, world, t1 - t0, dev)
+    per_rank = gather_per_rank(dist, world, t1 - t0, dev)
     value = world * per_rank_bytes * args.steps / elapsed / GIB
 
     # Roofline pass (after the timed region, not part of `value`): the scan
@@ -592,6 +664,7 @@ def main():
                   "chunk_params": "FASTCDC min 65536 / normal 1048576 / max 4194304",
                   "gear": "placeholder (v0.0.8 table unavailable; see DESIGN.md)",
                   "parallelism": f"independent buffers, 1 rank per GPU x {world}, no collective",
+                  "per_rank_gibs": [round(per_rank_bytes * args.steps / e / GIB, 2) for e in per_rank],
                   "chunks_per_step": nchunks}
         if host_mode:
             config["routed_bytes_per_gpu"] = routed_bytes

@@ -325,6 +325,16 @@ int cdc_set_debug_mode(int mode);
  * CDC_E_INVALID. */
 int cdc_set_maskl_index_mode(int mode);
 
+/* How a launch group finds its cut points: 0 = the full scan (every byte
+ * rolled by k_scan into a candidate index, then k_resolve), 2 = the skip walk
+ * (k_walk: each chain step scans only [p + Min, cut], as the reference's
+ * Algorithm reads only those bytes), 1 = adaptive (the skip walk while the
+ * data's chunks are mostly short of Normal, the full scan otherwise).  Cut
+ * points never depend on it.  Initial value from the CDC_WALK_MODE
+ * environment variable.  Not a reference interface.  Returns CDC_OK or
+ * CDC_E_INVALID. */
+int cdc_set_walk_mode(int mode);
+
 /* Adaptive MaskL state of one device (diagnostics, after a device sync):
  * *hint = 1 while the next launch groups build the MaskL index (a recent
  * group needed it), *groups = launch groups issued on the device so far.  Not a reference interface. */

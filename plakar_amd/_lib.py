@@ -140,6 +140,7 @@ SIGNATURES = {
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_set_walk_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_debug_maskl_state": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_uint32), _P(ctypes.c_uint64)]),
     "cdc_debug_set_digest_lanes": (ctypes.c_int, [ctypes.c_uint64]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),

@@ -99,6 +99,17 @@ std::atomic<uint32_t> &maskl_index_mode()
     return m;
 }
 
+// Walk mode (cdc_set_walk_mode; initial value from CDC_WALK_MODE): 0 the full
+// scan + index resolver, 2 the skip walk, 1 adaptive.
+std::atomic<uint32_t> &walk_mode()
+{
+    static std::atomic<uint32_t> m([] {
+        const char *e = getenv("CDC_WALK_MODE");
+        return e && (e[0] == '0' || e[0] == '1' || e[0] == '2') ? uint32_t(e[0] - '0') : 0u;
+    }());
+    return m;
+}
+
 uint64_t splitmix64(uint64_t &s)
 {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -274,10 +285,14 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     std::memset(&B, 0, sizeof(B));
     B.nbufs = uint32_t(n);
     B.final_ = final_ ? 1u : 0u;
-    B.total_segs = pl.total_segs;
-    B.total_tasks = pl.total_tasks;
-    B.seg = pl.seg;
+    const uint32_t wm = walk_mode().load(std::memory_order_relaxed);
+    B.skip = wm == 2 ? 1u : 0u;
+    B.total_segs = B.skip ? pl.total_segs_skip : pl.total_segs;
+    B.total_tasks = B.skip ? 0u : pl.total_tasks;
+    B.seg = B.skip ? pl.seg_skip : pl.seg;
     B.scan_lane = pl.scan_lane;
+    B.persist = pl.persist;
+    B.scan_wgs = pl.scan_wgs;
     static const uint32_t dbg = [] {
         const char *e = getenv("CDC_DEBUG_PHASE");
         return e ? uint32_t(atoi(e)) : 0u;
@@ -313,10 +328,10 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         D.cap = caps[i];
         D.res = res[i];
         D.seg_base = segs;
-        D.nseg = uint32_t((lens[i] + pl.seg - 1) / pl.seg);
+        D.nseg = uint32_t((lens[i] + B.seg - 1) / B.seg);
         D.task_base = tasks;
         segs += D.nseg;
-        tasks += uint32_t(align_tasks((lens[i] + 64ull * pl.scan_lane - 1) / (64ull * pl.scan_lane)));
+        tasks += uint32_t((lens[i] + 64ull * pl.scan_lane - 1) / (64ull * pl.scan_lane));
     }
     const Workspace W = carve(ws, pl, ctx->d_gear);
     return launch_batch(B, P, W, stream);
@@ -632,6 +647,13 @@ int cdc_validate(const char *algorithm, const cdc_opts *opts)
 int cdc_set_debug_mode(int mode)
 {
     G().debug_mode = mode;
+    return CDC_OK;
+}
+
+int cdc_set_walk_mode(int mode)
+{
+    if (mode < 0 || mode > 2) return CDC_E_INVALID;
+    walk_mode().store(uint32_t(mode), std::memory_order_relaxed);
     return CDC_OK;
 }
 

@@ -69,6 +69,9 @@ struct Batch {
     uint32_t *maskl_hint;    // mapped host word: set when some task needed the MaskL index
     uint32_t maskl_probe;    // 1: k_maskl_probe runs the selection test (adaptive mode, hint not set)
     uint64_t seg;            // resolution segment length in bytes
+    uint32_t skip;           // 1: the skip walk (k_walk, no scan, no index); 0: k_scan (+ MaskL) + k_resolve
+    uint32_t persist;        // 1: k_scan / k_scan_f run scan_wgs persistent workgroups pulling tasks
+    uint32_t scan_wgs;
     BufDesc b[kMaxBufsPerLaunch];
 };
 
@@ -91,17 +94,15 @@ struct Workspace {
 };
 
 struct Plan {
-    uint64_t seg;
+    uint64_t seg, seg_skip;  // resolution segment length: full-scan mode, skip walk
     uint32_t scan_lane;
-    uint32_t total_segs, total_tasks;
+    uint32_t total_segs, total_segs_skip, total_tasks;
+    uint32_t persist, scan_wgs;
     size_t off_runs, off_w1_nodes, off_xg, off_sg, off_flags, off_tick, off_runsL, off_validL,
         bytes;
 };
 
 // Host-side helpers implemented in cdc_kernels.hip.
-// Scan tasks of one buffer, rounded up so that every buffer starts on a scan
-// workgroup boundary (one buffer per workgroup: uniform stage alignment).
-uint64_t align_tasks(uint64_t tasks);
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan);
 int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *stream);
 // cdc_digest.hip: per-chunk SHA-256 (+ optional byte histogram) of device cut lists.

@@ -422,6 +422,11 @@ __device__ __forceinline__ void record_l_group(uint64_t f, const uint64_t (&g)[1
     }
 }
 
+template <bool kMaskL, bool kFused>
+__device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, const Workspace &W, char *s_lds,
+                                          const char *tab, uint32_t task, uint32_t lane, uint32_t wave,
+                                          uint32_t laneoff);
+
 // The byte scan.  kMaskL = false: the MaskS candidate index of every run
 // (k_scan).  kMaskL = true: the MaskL index (k_scan_l), built only for the
 // tasks maskl_needed() selects; every wave records validL for its task.
@@ -476,7 +481,35 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
                        uint32_t(__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11))));
     }
     const char *tab = s_lds;
-    if (task >= B.total_tasks || !act) return;
+    if (!act) return;
+    // Persistent mode (B.persist, k_scan / k_scan_f): one workgroup per CU;
+    // a wave's first task is static (blockIdx.x * kS2Waves + wave), later
+    // ones come from a per-launch atomic counter (W.tick[2], zeroed by the
+    // host before the launch), so CUs that run ahead (the end times spread by
+    // XCD, most at a cold clock) take more of the buffer.
+    const bool persist = !kMaskL && B.persist != 0;
+    const uint32_t nwaves = gridDim.x * kS2Waves;
+    for (uint32_t cur = task;;) {
+        if (cur >= B.total_tasks) break;
+        scan_task<kMaskL, kFused>(B, P, W, s_lds, tab, cur, lane, wave, laneoff);
+        if (!persist) break;
+        uint32_t t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(W.tick + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur = nwaves + uint32_t(__builtin_amdgcn_readfirstlane(t));
+    }
+    if (clk && threadIdx.x == 0) {
+        g_ts[clk + 2] = __builtin_amdgcn_s_memrealtime();
+        g_ts[clk + 3] = __builtin_amdgcn_s_memtime();
+    }
+}
+
+// One scan task: the 64 lane runs of task `task` (64 * B.scan_lane bytes of
+// one buffer), staged through this wave's LDS slot.
+template <bool kMaskL, bool kFused>
+__device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, const Workspace &W, char *s_lds,
+                                          const char *tab, uint32_t task, uint32_t lane, uint32_t wave,
+                                          uint32_t laneoff)
+{
     uint32_t b = 0;
     while (b + 1 < B.nbufs && task >= B.b[b + 1].task_base) ++b;
     const BufDesc &D = B.b[b];
@@ -642,10 +675,6 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
         if (lane == 0) W.validL[task] = 1u;
     }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
-    if (clk && threadIdx.x == 0) {
-        g_ts[clk + 2] = __builtin_amdgcn_s_memrealtime();
-        g_ts[clk + 3] = __builtin_amdgcn_s_memtime();
-    }
 }
 
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
@@ -796,6 +825,9 @@ struct WalkCtx {
     const uint64_t *gear;   // the 256-entry table in device memory
     const g_u64 *runsL;     // this buffer's MaskL index records (null: no MaskL index)
     const g_u32 *validL;    // per scan task of the buffer: runsL holds its 64 records
+    const lds_char *tab32;  // k_walk: 32-copy table in the MaskS frame (G << fs_sh), v_perm addresses
+    uint32_t laneoff32;     // (lane & 31) << 3
+    mutable uint32_t blocks;  // k_walk: skip_scan blocks of this wave (wave-uniform)
 };
 
 // (A 32-copy table for long raw scans, filled on first use: C3 +2-4 %, C1 -4 %
@@ -1035,6 +1067,179 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
         if (h != kNoHit) return h + P.cut_adj;
     }
     return clipped ? kUndet : p + n;
+}
+
+// ---------------------------------------------------------------------------
+// Skip walk (k_walk): next(p) from the bytes alone, no candidate index.
+//
+// The reference's Algorithm never reads [p, p + Min): it resets fp at
+// p + Min and stops at the first hit.  On random data with the default sizes a
+// chunk is ~96 KiB and the first hit lies ~32 KiB after p + Min, so a walker
+// that scans only [p + Min, cut] touches about a third of the bytes that the
+// full scan (k_scan) rolls, at the price of a sequential chain per resolution
+// segment (the junction / look-back of k_resolve make that chain parallel
+// across segments).  skip_scan is the wave's block scan: 64 lanes, each
+// rolling its own kSkipLane-byte slice after a 64-byte warm-up (reset at fz,
+// exactly as the reference), one ballot per block of 16 KiB.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSkipLane = 256;                           // bytes tested per lane per block
+constexpr uint32_t kSkipWarm = 64;                            // warm-up bytes (>= W - 1)
+constexpr uint32_t kSkipGroups = (kSkipLane + kSkipWarm) / 16;  // 16-B groups rolled per lane per block
+
+// Raw buffer resource over [base, base + bytes): reads past the end return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(uint64_t base, uint64_t bytes)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(base));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(base >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(uint32_t(bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : bytes));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, int(n),
+                                             0x00020000);
+}
+
+// Exact test of one 16-B group (offsets relative to the block base): fp before
+// the group, its 16 Gear values (MaskS frame); positions below fzr restart
+// the fingerprint at 0; returns the first hit in [tsr, ter) or ~0u, and
+// leaves fp exact after the group.
+template <bool kL>
+__device__ __forceinline__ uint32_t skip_exact(uint64_t &fp, const uint64_t (&g)[16], int32_t gr, int32_t tsr,
+                                               int32_t ter, int32_t fzr, const DevParams &P)
+{
+    uint64_t f = fp;
+    uint32_t hit = ~0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int32_t pos = gr + k;
+        f = pos < fzr ? 0ull : (f << 1) + g[k];
+        const uint32_t key = kL ? (__builtin_amdgcn_alignbit(uint32_t(f >> 32), uint32_t(f), P.fm_ws) & P.fm_m)
+                                : __builtin_amdgcn_bitop3_b32(uint32_t(f >> 32), P.fs_hi, uint32_t(f) & P.fs_lo, 0xEA);
+        if (hit == ~0u && key == 0 && pos >= tsr && pos < ter) hit = uint32_t(pos);
+    }
+    fp = f;
+    return hit;
+}
+
+// First position in [lo, hi) (buffer-relative) whose fingerprint, reset to 0
+// at fz <= lo, hits: MaskS (kL = false: the hi-dword filter of k_scan, then
+// the exact test) or MaskL (kL = true: its exact window in the MaskS frame,
+// P.fm_ok).  kNoHit if none.  lo >= Min >= 64, so the warm-up of the first
+// block stays inside the buffer's first 16-byte block.
+template <bool kL>
+__device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo, uint64_t hi, uint64_t fz)
+{
+    const uint32_t lane = C.lane;
+    const lds_char *tab = C.tab32;
+    const uint32_t laneoff = C.laneoff32;
+    const uint64_t FZ = C.ub + fz, H = C.ub + hi, END = C.ub + C.len;
+    const uint32_t vm = to_vgpr(kL ? P.fm_m : P.fs_hi);
+    const uint32_t lws = P.fm_ws;
+    const int32_t lo_off = int32_t(lane * kSkipLane);
+    uint64_t x = C.ub + lo;
+    while (x < H) {
+        const uint64_t A = x & ~15ull;
+        const uint64_t base = A - kSkipWarm;  // wave-uniform
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, END - base);
+        // this lane's tested range [tsr, ter) and the reset point, relative to base
+        const int32_t xr = int32_t(x - base);
+        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr);
+        const int32_t ter = int32_t(min<uint64_t>(uint64_t(lo_off) + kSkipWarm + kSkipLane, H - base));
+        const int32_t fzr = FZ >= base ? int32_t(FZ - base) : -1;
+        uint4 d[kSkipGroups];
+#pragma unroll
+        for (uint32_t i = 0; i < kSkipGroups; ++i)
+            d[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo_off + int32_t(16 * i), 0, 0));
+        uint64_t gv[2][16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
+        uint64_t fp = 0;
+        uint32_t hit = ~0u;
+#pragma unroll
+        for (uint32_t i = 0; i < kSkipGroups; ++i) {
+            uint64_t (&cg)[16] = gv[i & 1];
+            uint64_t (&ng)[16] = gv[(i + 1) & 1];
+            const uint4 nx = d[i + 1 < kSkipGroups ? i + 1 : i];
+            const uint64_t f0 = fp;
+            uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < 16; k += 2) {
+                const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
+                fp = (fp << 1) + cg[k];
+                if (i + 1 < kSkipGroups) ng[k] = lds_gear(tab, a0);
+                const uint32_t k0 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
+                                       : (uint32_t(fp >> 32) & vm);
+                const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
+                fp = (fp << 1) + cg[k + 1];
+                if (i + 1 < kSkipGroups) ng[k + 1] = lds_gear(tab, a1);
+                const uint32_t k1 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
+                                       : (uint32_t(fp >> 32) & vm);
+                acc = umin3(acc, k0, k1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const int32_t gr = lo_off + int32_t(16 * i);
+            bool chk = acc == 0 && gr + 16 > tsr && gr < ter;
+            if (i * 16 <= kSkipWarm) {  // the groups that can lie before the reset point
+                if (gr + 16 <= fzr) fp = 0;
+                chk = chk || (gr < fzr && gr + 16 > fzr);
+            }
+            if (chk && hit == ~0u) [[unlikely]] {
+                uint64_t f = f0;
+                hit = skip_exact<kL>(f, cg, gr, tsr, ter, fzr, P);
+                fp = f;
+            }
+        }
+        ++C.blocks;
+        const uint64_t m = __ballot(hit != ~0u);
+        if (m) return base + uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) - C.ub;
+        x = A + 64ull * kSkipLane;
+    }
+    return kNoHit;
+}
+
+// next_node() from the bytes alone (k_walk): the same window rules, every
+// candidate found by skip_scan (the truncated window included: skip_scan
+// restarts the fingerprint at fz).
+__device__ uint64_t next_node_skip(const WalkCtx &C, const DevParams &P, uint64_t p)
+{
+    const uint64_t E = C.len, r = E - p;
+    if (r <= P.min_size) return C.final_ ? E : kUndet;
+    uint64_t n, norm = P.normal_size, lim;
+    bool clipped = false;
+    if (C.final_) {
+        if (r >= P.max_size) {
+            n = P.max_size;
+        } else {
+            n = r;
+            if (r <= P.normal_size) norm = r;
+        }
+        lim = p + n;
+    } else {
+        n = P.max_size;
+        lim = p + n;
+        if (lim > E) {
+            lim = E;
+            clipped = true;
+        }
+    }
+    const uint64_t fz = p + P.min_size;
+    const uint64_t norm_end = p + norm;
+    const uint64_t s_end = min(norm_end, lim);
+    if (fz < s_end) {
+        const uint64_t h = skip_scan<false>(C, P, fz, s_end, fz);
+        if (h != kNoHit) return h + P.cut_adj;
+    }
+    const uint64_t l_lo = max(norm_end, fz);
+    if (l_lo < lim) {
+        const uint64_t h = P.fm_ok ? skip_scan<true>(C, P, l_lo, lim, fz)
+                                   : raw_first_hit(C, l_lo, lim, fz, P.ml_lo, P.ml_hi);
+        if (h != kNoHit) return h + P.cut_adj;
+    }
+    return clipped ? kUndet : p + n;
+}
+
+template <bool kSkip>
+__device__ __forceinline__ uint64_t next_of(const WalkCtx &C, const DevParams &P, uint64_t p)
+{
+    if constexpr (kSkip) return next_node_skip(C, P, p);
+    else return next_node(C, P, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -1334,6 +1539,9 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.gear = W.gear;
     C.runsL = B.maskl_index ? as_space<const g_u64>(reinterpret_cast<uintptr_t>(W.runsL + 64ull * D.task_base)) : nullptr;
     C.validL = B.maskl_index ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.validL + D.task_base)) : nullptr;
+    C.tab32 = nullptr;
+    C.laneoff32 = 0;
+    C.blocks = 0;
     return C;
 }
 
@@ -1562,11 +1770,12 @@ slow_path:  // q - 1's own INCLUSIVE status
 
 // The sequential walk of a whole buffer (debug mode, lists that overflow):
 // one wave walks next() from offset 0 and writes the cut list and the result row.
-__device__ void resolve_sequential(const WalkCtx &C, const DevParams &P, const BufDesc &D)
+template <bool kSkip>
+__device__ __forceinline__ void resolve_sequential(const WalkCtx &C, const DevParams &P, const BufDesc &D)
 {
     uint64_t p = 0, idx = 0;
     while (p < C.len) {
-        const uint64_t nx = next_node(C, P, p);
+        const uint64_t nx = next_of<kSkip>(C, P, p);
         if (nx == kUndet) break;
         if (C.lane == 0 && idx < D.cap) put_cut(D.out + idx, p, nx - p);
         ++idx;
@@ -1581,18 +1790,24 @@ __device__ void resolve_sequential(const WalkCtx &C, const DevParams &P, const B
     }
 }
 
+template <bool kSkip>
 __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams &P, const Workspace &W, uint32_t g,
-                                                const char *tab, GraphLds &L)
+                                                const char *tab, const char *tab32, GraphLds *L)
 {
     const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
-    const WalkCtx C = make_ctx(B, D, W, tab);
+    WalkCtx C = make_ctx(B, D, W, tab);
+    if constexpr (kSkip) {
+        C.tab32 = as_lds(tab32);
+        C.laneoff32 = (C.lane & 31u) << 3;
+    }
     const uint32_t lane = C.lane, base = D.seg_base, q = g - base;
     const uint64_t seg = B.seg, S0 = uint64_t(q) * seg, segE = S0 + seg, S1 = min(segE, C.len);
     const bool l0 = lane == 0;
     if (l0) dbg_ts(B, kTsRes + 8 * g);
     Graph G;
-    graph_build(C, P, L, G, S0, S1, B, kTsRes + 8 * g);
+    if constexpr (kSkip) G.n = kGNodes + 1;  // no index: every step is next_node_skip()
+    else graph_build(C, P, *L, G, S0, S1, B, kTsRes + 8 * g);
     if (l0) dbg_ts(B, kTsRes + 8 * g + 1);
     bool ovf = false;
     // ---- A (phase 0) and B (phase 1).  While the walk stays on listed nodes
@@ -1741,7 +1956,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 if (s != kGHard) {
                     nx = s;
                 } else {
-                    nx = next_node(C, P, x);
+                    nx = next_of<kSkip>(C, P, x);
                     ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
                     ++exact;
                 }
@@ -1805,7 +2020,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
         st_rlx(W.sg + g, kKindIncl | (uint64_t(Eq) << 38) | Oq);
         dbg_ts(B, kTsRes + 8 * g + 4);
         if (!(B.debug & kDbgGraph)) {
-            dbg_ts(B, kTsRes + 8 * g + 5, G.n);
+            dbg_ts(B, kTsRes + 8 * g + 5, kSkip ? C.blocks : G.n);
             dbg_ts(B, kTsRes + 8 * g + 6, exact);
             dbg_ts(B, kTsRes + 8 * g + 7, c2);
         }
@@ -1816,7 +2031,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
         for (uint32_t p = lane; p < q; p += 64)
             while ((ld_rlx(sgb + p) >> 62) != 2) __builtin_amdgcn_s_sleep(1);
         if (__hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || fb) {
-            resolve_sequential(C, P, D);
+            resolve_sequential<kSkip>(C, P, D);
             return;
         }
     }
@@ -1849,16 +2064,45 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B,
         }
     }
     const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(s_ticket)) * kWalkWavesPerWG + wave;
-    if (g < B.total_segs) resolve_segment(B, P, W, g, reinterpret_cast<const char *>(s_tab), s_graph[wave]);
+    if (g < B.total_segs)
+        resolve_segment<false>(B, P, W, g, reinterpret_cast<const char *>(s_tab), nullptr, &s_graph[wave]);
+}
+
+// The skip walk: k_resolve's phases over next_node_skip(), no scan kernel
+// before it (B.skip; the launch zeroes the granules with one memset).
+__global__ __launch_bounds__(kWalkWavesPerWG * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_walk(const Batch B, const DevParams P, const Workspace W)
+{
+    // 80 KiB of tables: two workgroups per CU.  Each wave takes its own
+    // ticket (no LDS word for a workgroup ticket: it would push the
+    // workgroup past half the CU's LDS).
+    __shared__ __attribute__((aligned(16))) uint64_t s_tab32[256 * 32];
+    __shared__ uint64_t s_tab[256 * kWCopies];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    uint32_t tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(W.tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(tk));
+    fill_gear_lds<kWalkWavesPerWG * 64, 32>(s_tab32, W.gear, P.fs_sh);
+    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
+    __syncthreads();
+    if (blockIdx.x == 0 && wave == 0) {
+        for (uint32_t i = lane; i < B.nbufs; i += 64) {
+            if (B.b[i].nseg == 0) {
+                B.b[i].res->ncuts = 0;
+                B.b[i].res->consumed = 0;
+                B.b[i].res->status = CDC_OK;
+                B.b[i].res->needed = 0;
+            }
+        }
+    }
+    if (g < B.total_segs)
+        resolve_segment<true>(B, P, W, g, reinterpret_cast<const char *>(s_tab),
+                              reinterpret_cast<const char *>(s_tab32), nullptr);
 }
 
 // ---------------------------------------------------------------------------
 // Host side: planning and launching.
 // ---------------------------------------------------------------------------
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-// Scan tasks of one buffer (a workgroup's waves may belong to different buffers).
-uint64_t align_tasks(uint64_t t) { return t; }
 
 int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
 {
@@ -1879,6 +2123,15 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     if (seg < need) seg = need;
     seg = (seg + 15) & ~15ull;
     plan->seg = seg;
+    // Skip-walk segments (k_walk): 8 Min (512 KiB at the defaults), two walker
+    // waves per SIMD on a 1-GiB buffer.  Every step of a walk scans bytes, so a
+    // segment is a trade between chain parallelism and the junction (about 1.4
+    // extra steps per segment on random data).
+    uint64_t smult = 8;
+    uint64_t seg_skip = smult * P.min_size;
+    if (seg_skip < need) seg_skip = need;
+    seg_skip = (seg_skip + 15) & ~15ull;
+    plan->seg_skip = seg_skip;
     // Scan lane length: one scan workgroup per CU (a workgroup holds 112 KiB of
     // LDS), for a grid of at most CUs - 7 workgroups; lane lengths are
     // multiples of 256 B (odd multiples of 128 B ran slower), so 1 GiB takes
@@ -1895,12 +2148,23 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
             n = 256;
         return uint64_t(n);
     }();
-    uint64_t wgs = cus > 16 ? cus - 7 : cus;
+    // Persistent scan (default): one workgroup per CU pulling tasks of 64
+    // lane runs from a counter, about kTasksPerWave tasks per wave, so that
+    // the CUs that run ahead take the tail.
+    static const uint64_t persist_tpw = [] {
+        const char *e = getenv("CDC_SCAN_TASKS_PER_WAVE");  // 0: static grid (one task per wave)
+        const long v = e ? atol(e) : 3;
+        return uint64_t(v >= 0 && v <= 64 ? v : 3);
+    }();
+    uint64_t wgs = persist_tpw ? cus : (cus > 16 ? cus - 7 : cus);
     if (const char *env = getenv("CDC_SCAN_WGS")) {
         const long v = atol(env);
         if (v >= 1 && v <= 65536) wgs = uint64_t(v);
     }
-    uint64_t want = (total + wgs * kS2Waves * 64 - 1) / (wgs * kS2Waves * 64);
+    const uint64_t tpw = persist_tpw ? persist_tpw : 1;
+    plan->persist = persist_tpw ? 1u : 0u;
+    plan->scan_wgs = uint32_t(wgs);
+    uint64_t want = (total + wgs * kS2Waves * 64 * tpw - 1) / (wgs * kS2Waves * 64 * tpw);
     want = (want + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
     if (want < 512) want = (512 + kLaneQuant - 1) / kLaneQuant * kLaneQuant;
     if (want > kScanLaneBytes) want = kScanLaneBytes / kLaneQuant * kLaneQuant;
@@ -1911,7 +2175,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
         for (int i = 0; i < nbufs; ++i) t += (lens[i] + 64 * ln - 1) / (64 * ln);
         return (t + kS2Waves - 1) / kS2Waves;
     };
-    while (want + kLaneQuant <= kScanLaneBytes && grid_of(want) > wgs) want += kLaneQuant;
+    while (want + kLaneQuant <= kScanLaneBytes && grid_of(want) > wgs * tpw) want += kLaneQuant;
     uint32_t lane = uint32_t(want);
     if (const char *env = getenv("CDC_SCAN_LANE_BYTES")) {
         const long v = atol(env);
@@ -1919,14 +2183,17 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     }
     plan->scan_lane = lane;
     const uint64_t task_bytes = 64ull * lane;
-    uint64_t segs = 0, tasks = 0;
+    uint64_t segs = 0, segs_skip = 0, tasks = 0;
     for (int i = 0; i < nbufs; ++i) {
         segs += (lens[i] + seg - 1) / seg;
-        tasks += align_tasks((lens[i] + task_bytes - 1) / task_bytes);
+        segs_skip += (lens[i] + seg_skip - 1) / seg_skip;
+        tasks += (lens[i] + task_bytes - 1) / task_bytes;
     }
-    if (segs >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
+    if (segs >= 0xFFFF0000ull || segs_skip >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
     plan->total_segs = uint32_t(segs);
+    plan->total_segs_skip = uint32_t(segs_skip);
     plan->total_tasks = uint32_t(tasks);
+    if (segs_skip > segs) segs = segs_skip;  // the per-segment arrays serve either mode
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -1938,7 +2205,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_xg = take(segs * 8);
     plan->off_sg = take(segs * 8);
     plan->off_flags = take(kMaxBufsPerLaunch * 4);
-    plan->off_tick = take(2 * 4);
+    plan->off_tick = take(4 * 4);  // [0] k_resolve / k_walk ticket, [2] persistent scan task counter
     plan->off_runsL = take(tasks * 64 * 8);
     plan->off_validL = take(tasks * 4);
     plan->bytes = off;
@@ -1978,10 +2245,26 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     for (uint32_t i = 0; i < B.nbufs; ++i) bytes += B.b[i].len;
     ProfRec pr;
     const bool prof = prof_begin(pr, bytes);
+    if (B.skip) {  // the skip walk: granules zeroed, then one kernel
+        const size_t zb = size_t(reinterpret_cast<char *>(W.tick + 2) - reinterpret_cast<char *>(W.xg));
+        if (hipMemsetAsync(W.xg, 0, zb, st) != hipSuccess) return CDC_E_DEVICE;
+        const dim3 rgrid(B.total_segs > 0 ? (B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG : 1u);
+        if (prof) {
+            hipExtLaunchKernelGGL(k_walk, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            (void)hipEventRecord(pr.e2, st);
+            g_prof_live.push_back(pr);
+        } else {
+            hipLaunchKernelGGL(k_walk, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
+        }
+        return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+    }
     // With profiling on, the events ride on the kernels' own dispatch packets
     // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
-    const dim3 sgrid((B.total_tasks + kS2Waves - 1) / kS2Waves), sblock(kS2Waves * 64);
+    const uint32_t need_wgs = (B.total_tasks + kS2Waves - 1) / kS2Waves;
+    const dim3 sgrid(B.persist && B.scan_wgs < need_wgs ? B.scan_wgs : need_wgs), sblock(kS2Waves * 64);
     const bool fused = B.maskl_index && B.maskl_fused;  // k_scan_f: both indexes in one pass
+    if (B.persist && B.total_tasks > 0 && hipMemsetAsync(W.tick + 2, 0, 4, st) != hipSuccess) return CDC_E_DEVICE;
     if (B.total_tasks == 0) {  // every buffer is empty
         if (prof) {
             (void)hipEventRecord(pr.e0, st);
@@ -2013,7 +2296,7 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     // MaskL index of the tasks near long MaskS-free stretches (most workgroups
     // exit after one look at the MaskS index on ordinary data)
     if (B.total_tasks > 0 && B.maskl_index && !fused)
-        hipLaunchKernelGGL(k_scan_l, sgrid, sblock, 0, st, B, P, W);
+        hipLaunchKernelGGL(k_scan_l, dim3(need_wgs), sblock, 0, st, B, P, W);  // not persistent (workgroup vote)
     else if (B.total_tasks > 0 && B.maskl_probe)
         hipLaunchKernelGGL(k_maskl_probe, dim3((B.total_tasks + kProbeWaves - 1) / kProbeWaves), dim3(kProbeWaves * 64),
                            0, st, B, P, W);

@@ -62,3 +62,38 @@ def test_c2_shards_cover_baseline_config():
     wl = bench.WORKLOADS["c2"]
     seeds = [s for r in range(8) for s in bench.buffer_seeds(wl, r, 8)]
     assert len(set(seeds)) == 256 and wl["size"] == 64 << 20
+
+
+def _run_bench(args, extra_env):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(extra_env)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_spawns_its_own_ranks(n):
+    """`python bench.py --gpus N` with no launcher starts N rank processes
+    (gloo rendezvous on 127.0.0.1) and reports n_gpus = N with one timing per
+    rank; BENCH_CPU_SELFTEST runs the plumbing without a GPU."""
+    rc, line, err = _run_bench(["--gpus", str(n)], {"BENCH_CPU_SELFTEST": "1"})
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == n and line["selftest"]
+    assert len(line["per_rank_elapsed_s"]) == n
+    # the max over ranks is the slowest rank's time (rank r sleeps (r + 1) * 10 ms)
+    assert line["elapsed_max_s"] == max(line["per_rank_elapsed_s"])
+    assert line["per_rank_elapsed_s"][-1] >= 0.01 * n
+
+
+def test_bench_refuses_a_mismatched_launcher():
+    """A launcher that started a different number of ranks than --gpus asks
+    for is an error, never a silent 1-rank run."""
+    rc, line, err = _run_bench(["--gpus", "2"], {"BENCH_CPU_SELFTEST": "1", "WORLD_SIZE": "1", "RANK": "0"})
+    assert rc != 0 and line is None
+    assert "WORLD_SIZE=1" in err

@@ -99,6 +99,22 @@ def test_two_ranks_c2_shares_on_one_gpu():
     assert d["ranks"] == 2 and d["buffers"] == 64 and d["mismatched_buffers"] == 0, d
 
 
+def test_bench_spawns_two_ranks_on_one_gpu():
+    """`python bench.py --gpus 2` with no launcher (the form the driver uses
+    for BENCH) starts two rank processes itself; BENCH_REHEARSE_ONE_GPU puts
+    both on device 0 over gloo.  The line reports both ranks."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_REHEARSE_ONE_GPU"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--size-mib", "64", "--no-cpu-baseline", "--digest-reps", "0", "--encode-reps", "0", "--e2e-reps", "0"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and len(d["config"]["per_rank_gibs"]) == 2, d
+    assert d["config"]["global_bytes"] == 2 * d["config"]["bytes_per_gpu"]
+
+
 def test_sequential_fallback_cost_1GiB(oracle):
     """The sequential fallback (debug mode 1 forces it) on a 1 GiB buffer: the
     cliff a buffer whose speculative chains never merge would hit.  Bit-exact,
