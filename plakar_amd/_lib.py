@@ -6,6 +6,7 @@ command that builds it.
 """
 import ctypes
 import os
+import sys
 import warnings
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -161,12 +162,16 @@ def lib():
                 "(build it with `python -m plakar_amd.build`); there is no CPU fallback")
         # With PyTorch in the process there are two HIP runtimes (torch's bundled
         # one and the system's, which this library links); torch's must come up
-        # first, or torch then finds no device.
-        try:
-            import torch
-            torch.cuda.is_available()
-        except Exception:
-            pass
+        # first, or torch then finds no device.  Only when torch is already
+        # imported is its runtime brought up here: loading the library never
+        # imports torch itself (the modules that use torch tensors -- device,
+        # hashing, snapshot, encode -- import it before they load the library).
+        torch = sys.modules.get("torch")
+        if torch is not None:
+            try:
+                torch.cuda.is_available()
+            except Exception:
+                pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             if os.environ.get("PLAKAR_CDC_LIB") and not hasattr(L, name):

@@ -590,6 +590,137 @@ int run_host_jobs(DeviceCtx *ctx, const cdc_opts *o, std::vector<HostJob *> &job
 
 }  // namespace
 
+namespace cdc {
+
+int device_count_initialised()
+{
+    Global &g = G();
+    return g.init.load(std::memory_order_acquire) ? int(g.devs.size()) : 0;
+}
+
+// The collector's per-device worker (see cdc_internal.h): run_host_jobs'
+// two-slot pipeline, fed batch by batch for as long as the source has work.
+// The device lock is held while groups are in flight and released whenever
+// the pipeline drains, so other callers of the device interleave at idle
+// points.  A failing batch is handed back with the status on every buffer.
+int pipeline_device(int di, const cdc_opts *o, BatchSource &src)
+{
+    Global &g = G();
+    if (!g.init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
+    if (di < 0 || size_t(di) >= g.devs.size()) return CDC_E_INVALID;
+    DeviceCtx *ctx = g.devs[size_t(di)];
+    const DevParams P = make_params(o);
+    const uint64_t budget = std::max<uint64_t>(env_mb("CDC_HOST_GROUP_MB", 1024, 16), 4ull * o->max_size + 4096);
+    const uint64_t maxbuf = std::max<uint64_t>(env_mb("CDC_HOST_MAXBUF_MB", 16384, 16), budget);
+    std::unique_lock<std::mutex> lock(ctx->mu, std::defer_lock);
+    std::vector<HostBuf *> fl[2];
+    std::vector<uint64_t> cut_off[2];
+    bool active[2] = {false, false};
+    auto fail = [&](std::vector<HostBuf *> &b, int st) {
+        for (HostBuf *h : b) h->status = st;
+        src.finished(b);
+        b.clear();
+    };
+    auto harvest = [&](int s) {
+        if (!active[s]) return;
+        active[s] = false;
+        Slot &sl = ctx->slot[s];
+        int st = hipEventSynchronize(sl.done) == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+        for (size_t i = 0; i < fl[s].size(); ++i) {
+            HostBuf *h = fl[s][i];
+            const cdc_result r = sl.h_res[i];
+            h->status = st != CDC_OK ? st : int(r.status);
+            if (h->status == CDC_OK) h->cuts.assign(sl.h_cuts + cut_off[s][i], sl.h_cuts + cut_off[s][i] + r.ncuts);
+        }
+        src.finished(fl[s]);
+        fl[s].clear();
+    };
+    // stage + launch one batch into slot s (one launch group; a buffer over
+    // maxbuf goes through the windowed path synchronously)
+    auto submit = [&](int s, std::vector<HostBuf *> &b) -> int {
+        if (b.size() == 1 && b[0]->len > maxbuf) {
+            HostJob job{b[0]->data, b[0]->len, {}, CDC_OK};
+            const int st = run_windowed(ctx, P, o, &job, budget);
+            b[0]->status = st;
+            if (st == CDC_OK) b[0]->cuts = std::move(job.cuts);
+            src.finished(b);
+            b.clear();
+            return CDC_OK;
+        }
+        const int n = int(b.size());
+        std::vector<uint64_t> offs(n), lens(n), caps(n);
+        cut_off[s].assign(n, 0);
+        uint64_t used = 0, ncuts = 0;
+        for (int i = 0; i < n; ++i) {
+            offs[i] = used;
+            lens[i] = b[i]->len;
+            caps[i] = max_cuts_for(b[i]->len, o->min_size);
+            cut_off[s][i] = ncuts;
+            ncuts += caps[i];
+            used = (used + b[i]->len + 255) & ~255ull;
+        }
+        Slot &sl = ctx->slot[s];
+        uint64_t need = 0;
+        int st = group_ws_bytes(lens.data(), n, P, &need);
+        if (st != CDC_OK) return st;
+        if ((st = grow_slot(sl, std::max<uint64_t>(used, 256), need, ncuts)) != CDC_OK) return st;
+        for (int i = 0; i < n; ++i)
+            if (lens[i] && (st = stage(ctx, sl.d_in + offs[i], b[i]->data, lens[i])) != CDC_OK) return st;
+        HIPCHK(hipEventRecord(sl.staged, ctx->copy));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, sl.staged, 0));
+        std::vector<const void *> dp(n);
+        std::vector<cdc_cut *> cp(n);
+        std::vector<cdc_result *> rp(n);
+        for (int i = 0; i < n; ++i) {
+            dp[i] = sl.d_in + offs[i];
+            cp[i] = sl.d_cuts + cut_off[s][i];
+            rp[i] = sl.d_res + i;
+        }
+        st = run_group(ctx, P, dp.data(), lens.data(), n, 1, cp.data(), caps.data(), rp.data(), sl.d_ws, sl.ws_cap,
+                       ctx->stream);
+        if (st != CDC_OK) return st;
+        HIPCHK(hipMemcpyAsync(sl.h_res, sl.d_res, n * sizeof(cdc_result), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(sl.h_cuts, sl.d_cuts, ncuts * sizeof(cdc_cut), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipEventRecord(sl.done, ctx->stream));
+        fl[s] = std::move(b);
+        active[s] = true;
+        return CDC_OK;
+    };
+    int cur = 0;
+    for (;;) {
+        const bool busy = active[0] || active[1];
+        if (!busy && lock.owns_lock()) lock.unlock();  // drained: other callers may use the device
+        std::vector<HostBuf *> batch;
+        if (!src.next(batch, !busy)) {
+            if (!busy) return CDC_OK;  // the source is stopping
+            harvest(active[cur] ? cur : cur ^ 1);  // the older group first (cur is the slot used next)
+            continue;
+        }
+        if (batch.empty()) continue;
+        if (!lock.owns_lock()) {
+            lock.lock();
+            int st = hipSetDevice(ctx->device) == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+            if (st == CDC_OK && !ctx->copy && hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking) != hipSuccess)
+                st = CDC_E_DEVICE;
+            if (st == CDC_OK) st = grow_bounce(ctx, std::min<uint64_t>(64ull << 20, budget));
+            if (st != CDC_OK) {
+                fail(batch, st);
+                continue;
+            }
+        }
+        const int s = cur;
+        cur ^= 1;
+        harvest(s);  // the slot's previous group
+        const int st = submit(s, batch);
+        if (st != CDC_OK) {
+            fail(batch, st);
+            harvest(s ^ 1);
+        }
+    }
+}
+
+}  // namespace cdc
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -784,8 +915,14 @@ int cdc_init(uint32_t dev_mask, const uint64_t gear[256], uint64_t mask_s, uint6
     for (auto *c : g.devs) {
         if (hipSetDevice(c->device) != hipSuccess ||
             hipMemcpy(c->d_gear, g.gear, sizeof(g.gear), hipMemcpyHostToDevice) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess)
+            hipDeviceSynchronize() != hipSuccess) {
+            // a partial update would leave devices on different tables: tear
+            // everything down, so a failed cdc_init leaves the library
+            // uninitialised with nothing allocated (the header's contract)
+            for (auto *d : g.devs) destroy_ctx(d);
+            g.devs.clear();
             return CDC_E_DEVICE;
+        }
     }
     g.init.store(true, std::memory_order_release);
     return CDC_OK;
@@ -1012,6 +1149,18 @@ static int read_full(int fd, uint8_t *dst, uint64_t len)
     return CDC_OK;
 }
 
+// One file into its reserved slot: open, read exactly len bytes, close.  Each
+// reader thread holds at most one descriptor, so a batch of any number of
+// files stays within RLIMIT_NOFILE.
+static int read_path(const char *path, uint8_t *dst, uint64_t len)
+{
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return CDC_E_IO;
+    const int st = read_full(fd, dst, len);
+    close(fd);
+    return st;
+}
+
 extern "C" int cdc_batch_add_fd(cdc_batch *b, int fd, uint64_t len)
 {
     uint8_t *p = nullptr;
@@ -1030,18 +1179,14 @@ extern "C" int cdc_batch_add_files(cdc_batch *b, const char *const *paths, int n
     if (!b || n < 0 || (n > 0 && !paths)) return CDC_E_INVALID;
     const size_t first = b->bufs.size();
     const uint64_t used0 = b->used;
-    std::vector<int> fds(size_t(n), -1);
     auto undo = [&](int st) {
-        for (int fd : fds)
-            if (fd >= 0) close(fd);
         b->bufs.resize(first);
         b->used = used0;
         return st;
     };
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i) {  // sizes by stat(): no descriptor is held across the batch
         struct stat sb;
-        fds[size_t(i)] = open(paths[i], O_RDONLY | O_CLOEXEC);
-        if (fds[size_t(i)] < 0 || fstat(fds[size_t(i)], &sb) != 0) return undo(CDC_E_IO);
+        if (!paths[i] || stat(paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) return undo(CDC_E_IO);
         uint8_t *p = nullptr;
         const int st = cdc_batch_reserve(b, uint64_t(sb.st_size), &p);
         if (st != CDC_OK) return undo(st);
@@ -1050,21 +1195,21 @@ extern "C" int cdc_batch_add_files(cdc_batch *b, const char *const *paths, int n
     const int nt = std::max(1, std::min(threads, n));
     std::atomic<int> next{0}, err{CDC_OK};
     auto work = [&] {
-        for (int i; (i = next.fetch_add(1)) < n;) {
+        for (int i; (i = next.fetch_add(1)) < n && err.load() == CDC_OK;) {
             const cdc_buf &cb = b->bufs[first + size_t(i)];
-            const int st = read_full(fds[size_t(i)], static_cast<uint8_t *>(const_cast<void *>(cb.data)), cb.len);
+            const int st = read_path(paths[i], static_cast<uint8_t *>(const_cast<void *>(cb.data)), cb.len);
             if (st != CDC_OK) err.store(st);
         }
     };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-    work();
-    for (auto &t : pool) t.join();
-    if (err.load() != CDC_OK) return undo(err.load());
-    for (int &fd : fds) {
-        close(fd);
-        fd = -1;
+    try {
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+        work();
+        for (auto &t : pool) t.join();
+    } catch (...) {
+        return undo(CDC_E_NOMEM);
     }
+    if (err.load() != CDC_OK) return undo(err.load());
     return CDC_OK;
 }
 
@@ -1085,20 +1230,16 @@ extern "C" int cdc_batch_chunk_files(cdc_batch *b, const char *const *paths, int
     if (!G().init.load(std::memory_order_acquire)) return CDC_E_NOT_INIT;
     const size_t first = b->bufs.size();
     const uint64_t used0 = b->used;
-    std::vector<int> fds(size_t(n), -1);
     auto undo = [&](int st) {
-        for (int fd : fds)
-            if (fd >= 0) close(fd);
         b->bufs.resize(first);
         b->used = used0;
         return st;
     };
     std::vector<int> sub_end;  // file index one past each sub-batch
     uint64_t acc = 0;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i) {  // sizes by stat(); readers open, read and close one file at a time
         struct stat sb;
-        fds[size_t(i)] = open(paths[i], O_RDONLY | O_CLOEXEC);
-        if (fds[size_t(i)] < 0 || fstat(fds[size_t(i)], &sb) != 0) return undo(CDC_E_IO);
+        if (!paths[i] || stat(paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) return undo(CDC_E_IO);
         uint8_t *p = nullptr;
         const int st = cdc_batch_reserve(b, uint64_t(sb.st_size), &p);
         if (st != CDC_OK) return undo(st);
@@ -1120,7 +1261,7 @@ extern "C" int cdc_batch_chunk_files(cdc_batch *b, const char *const *paths, int
     auto work = [&] {
         for (int i; (i = next.fetch_add(1)) < n && err.load() == CDC_OK;) {
             const cdc_buf &cb = b->bufs[first + size_t(i)];
-            const int st = read_full(fds[size_t(i)], static_cast<uint8_t *>(const_cast<void *>(cb.data)), cb.len);
+            const int st = read_path(paths[i], static_cast<uint8_t *>(const_cast<void *>(cb.data)), cb.len);
             if (st != CDC_OK) err.store(st);
             std::lock_guard<std::mutex> lk(mu);
             --left[size_t(sub_of[size_t(i)])];
@@ -1131,7 +1272,13 @@ extern "C" int cdc_batch_chunk_files(cdc_batch *b, const char *const *paths, int
     };
     const int nt = std::max(1, std::min(threads, n));
     std::vector<std::thread> pool;
-    for (int t = 0; t < nt; ++t) pool.emplace_back(work);
+    try {
+        for (int t = 0; t < nt; ++t) pool.emplace_back(work);
+    } catch (...) {
+        err.store(CDC_E_NOMEM);
+        for (auto &t : pool) t.join();
+        return undo(CDC_E_NOMEM);
+    }
     int status = CDC_OK;
     uint64_t k = 0, needed = 0;
     for (size_t j = 0; j < sub_end.size() && status != CDC_E_IO; ++j) {
@@ -1156,10 +1303,6 @@ extern "C" int cdc_batch_chunk_files(cdc_batch *b, const char *const *paths, int
     if (status != CDC_OK && status != CDC_E_NOSPACE) err.store(status);  // readers stop early
     for (auto &t : pool) t.join();
     if (err.load() != CDC_OK) return undo(err.load());
-    for (int &fd : fds) {
-        close(fd);
-        fd = -1;
-    }
     if (out_needed) *out_needed = needed;
     return status;
 }

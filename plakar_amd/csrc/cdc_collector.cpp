@@ -4,18 +4,24 @@
 // snapshot/backup.go:216-225, up to NumCPU x 8 + 1 at once, each running the
 // per-file Next() loop of snapshot/backup.go:647-665).  One launch group per
 // file would leave the GPU mostly idle on small files and pay a PCIe round
-// trip per call.  A collector takes those calls from any number of threads,
-// queues them, and a worker thread hands them to the device as batches: a
-// batch closes when its bytes reach batch_bytes, when it holds 64 files, or
-// max_wait_us after its first file arrived.  Each batch is one cdc_chunk call
-// (LPT over the devices, pipelined H2D); every caller blocks until its own cut
-// list is back, so the calling contract is the synchronous one of cdc_chunk
-// for one buffer.
+// trip per call.  A collector takes those calls from any number of threads
+// and queues them; one worker per device pulls batches from the shared queue
+// (dynamic balance across devices) and runs them through a two-slot pipeline
+// that outlives a batch (cdc::pipeline_device): batch k + 1 is staged (H2D)
+// while batch k is chunked, and batch k's cut lists come back while k + 1
+// runs.  A batch closes when its bytes reach batch_bytes, when it holds
+// kMaxBufsPerLaunch files, or max_wait_us after its first file arrived (the
+// wait applies while the device is idle; with a batch in flight a closed
+// batch is taken as soon as it is closed).  Every caller blocks until its own
+// cut list is back: the calling contract is the synchronous one of cdc_chunk
+// for one buffer.  No C++ exception crosses the C ABI.
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -23,102 +29,109 @@
 
 namespace {
 
-struct Request {
-    const void *data;
-    uint64_t len;
+struct Request : cdc::HostBuf {
     cdc_cut *out;
     uint64_t cap;
     uint64_t count = 0;
-    int status = CDC_OK;
     bool done = false;
 };
 
-constexpr size_t kMaxBatchFiles = 64;
+constexpr size_t kMaxBatchFiles = cdc::kMaxBufsPerLaunch;
 
 }  // namespace
 
-struct cdc_collector {
+struct cdc_collector final : cdc::BatchSource {
     cdc_opts opts;
     uint64_t batch_bytes;
     std::chrono::microseconds max_wait;
     std::mutex mu;
-    std::condition_variable cv_work;  // worker: a request arrived / shutting down
-    std::condition_variable cv_done;  // callers: a batch finished
+    std::condition_variable cv_work;  // workers: a request arrived / shutting down
+    std::condition_variable cv_done;  // callers: a batch finished; free(): the last caller left
     std::deque<Request *> queue;
     uint64_t queued_bytes = 0;
     std::chrono::steady_clock::time_point first_arrival;
     bool stop = false;
     uint64_t n_requests = 0, n_batches = 0;
-    std::thread worker;
+    uint64_t callers = 0;  // threads inside cdc_collector_chunk
+    std::vector<std::thread> workers;
 
-    void run();
-};
+    bool closed(std::chrono::steady_clock::time_point now) const
+    {
+        return stop || queued_bytes >= batch_bytes || queue.size() >= kMaxBatchFiles || now >= first_arrival + max_wait;
+    }
 
-void cdc_collector::run()
-{
-    std::vector<Request *> batch;
-    std::vector<cdc_buf> bufs;
-    std::vector<uint64_t> counts;
-    std::vector<cdc_cut> cuts;
-    for (;;) {
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            for (;;) {
-                if (queue.empty()) {
-                    if (stop) return;
-                    cv_work.wait(lk);
-                    continue;
-                }
-                if (stop || queued_bytes >= batch_bytes || queue.size() >= kMaxBatchFiles) break;
-                const auto deadline = first_arrival + max_wait;
-                if (std::chrono::steady_clock::now() >= deadline) break;
-                cv_work.wait_until(lk, deadline);
+    bool next(std::vector<cdc::HostBuf *> &batch, bool wait) override
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            if (queue.empty()) {
+                if (stop || !wait) return false;
+                cv_work.wait(lk);
+                continue;
             }
-            batch.clear();
-            uint64_t bytes = 0;
-            while (!queue.empty() && batch.size() < kMaxBatchFiles && (batch.empty() || bytes < batch_bytes)) {
-                batch.push_back(queue.front());
-                bytes += queue.front()->len;
-                queue.pop_front();
-            }
-            queued_bytes -= bytes;
-            if (!queue.empty()) first_arrival = std::chrono::steady_clock::now();
-            ++n_batches;
+            const auto now = std::chrono::steady_clock::now();
+            if (closed(now)) break;
+            if (!wait) return false;
+            cv_work.wait_until(lk, first_arrival + max_wait);
         }
-        // one cdc_chunk over the batch: cut lists into a scratch array sized by
-        // the bound len / Min + 2 per buffer, then copied to each caller
-        bufs.resize(batch.size());
-        counts.assign(batch.size(), 0);
-        uint64_t cap = 0;
-        for (size_t i = 0; i < batch.size(); ++i) {
-            bufs[i].data = batch[i]->data;
-            bufs[i].len = batch[i]->len;
-            cap += batch[i]->len / (opts.min_size ? opts.min_size : 1) + 2;
+        uint64_t bytes = 0;
+        while (!queue.empty() && batch.size() < kMaxBatchFiles && (batch.empty() || bytes + queue.front()->len <= batch_bytes)) {
+            batch.push_back(static_cast<cdc::HostBuf *>(queue.front()));
+            bytes += queue.front()->len;
+            queue.pop_front();
         }
-        cuts.resize(cap);
-        uint64_t needed = 0;
-        const int st = cdc_chunk(bufs.data(), int(bufs.size()), &opts, cuts.data(), cap, counts.data(), &needed);
+        queued_bytes -= bytes;
+        if (!queue.empty()) first_arrival = std::chrono::steady_clock::now();
+        ++n_batches;
+        return true;
+    }
+
+    void finished(std::vector<cdc::HostBuf *> &batch) override
+    {
         {
             std::lock_guard<std::mutex> lk(mu);
-            uint64_t k = 0;
-            for (size_t i = 0; i < batch.size(); ++i) {
-                Request *r = batch[i];
-                r->count = counts[i];
-                if (st != CDC_OK) {
-                    r->status = st;
-                } else if (counts[i] > r->cap || (counts[i] && !r->out)) {
-                    r->status = CDC_E_NOSPACE;
-                } else {
-                    if (counts[i]) std::memcpy(r->out, cuts.data() + k, counts[i] * sizeof(cdc_cut));
-                    r->status = CDC_OK;
+            for (cdc::HostBuf *h : batch) {
+                Request *r = static_cast<Request *>(h);
+                r->count = h->cuts.size();
+                if (h->status != CDC_OK) {
+                    r->count = 0;
+                } else if (r->count > r->cap || (r->count && !r->out)) {
+                    h->status = CDC_E_NOSPACE;
+                } else if (r->count) {
+                    std::memcpy(r->out, h->cuts.data(), r->count * sizeof(cdc_cut));
                 }
-                k += counts[i];
                 r->done = true;
             }
         }
         cv_done.notify_all();
     }
-}
+
+    void fail_all(int st)  // a worker could not run: nobody may wait forever
+    {
+        std::vector<cdc::HostBuf *> b;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (Request *r : queue) b.push_back(r);
+            queue.clear();
+            queued_bytes = 0;
+        }
+        for (cdc::HostBuf *h : b) h->status = st;
+        if (!b.empty()) finished(b);
+    }
+
+    void run(int dev)
+    {
+        int st;
+        try {
+            st = cdc::pipeline_device(dev, &opts, *this);
+        } catch (const std::bad_alloc &) {
+            st = CDC_E_NOMEM;
+        } catch (...) {
+            st = CDC_E_DEVICE;
+        }
+        if (st != CDC_OK) fail_all(st);
+    }
+};
 
 extern "C" {
 
@@ -127,11 +140,25 @@ int cdc_collector_new(const cdc_opts *opts, uint64_t batch_bytes, uint32_t max_w
     if (!opts || !out) return CDC_E_INVALID;
     const int v = cdc_validate("fastcdc", opts);
     if (v != CDC_OK) return v;
-    auto *c = new cdc_collector();
+    const int ndev = cdc::device_count_initialised();
+    if (ndev <= 0) return CDC_E_NOT_INIT;
+    auto *c = new (std::nothrow) cdc_collector();
+    if (!c) return CDC_E_NOMEM;
     c->opts = *opts;
     c->batch_bytes = batch_bytes ? batch_bytes : (256ull << 20);
     c->max_wait = std::chrono::microseconds(max_wait_us);
-    c->worker = std::thread([c] { c->run(); });
+    try {
+        for (int d = 0; d < ndev; ++d) c->workers.emplace_back([c, d] { c->run(d); });
+    } catch (...) {
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            c->stop = true;
+        }
+        c->cv_work.notify_all();
+        for (auto &t : c->workers) t.join();
+        delete c;
+        return CDC_E_NOMEM;
+    }
     *out = c;
     return CDC_OK;
 }
@@ -143,19 +170,32 @@ int cdc_collector_chunk(cdc_collector *c, const void *data, uint64_t len, cdc_cu
                         uint64_t *count)
 {
     if (!c || !count || (len && !data)) return CDC_E_INVALID;
-    Request r{data, len, out, cap};
-    {
-        std::unique_lock<std::mutex> lk(c->mu);
-        if (c->stop) return CDC_E_INVALID;
+    Request r;
+    r.data = static_cast<const uint8_t *>(data);
+    r.len = len;
+    r.status = CDC_OK;
+    r.out = out;
+    r.cap = cap;
+    std::unique_lock<std::mutex> lk(c->mu);
+    if (c->stop) return CDC_E_INVALID;
+    ++c->callers;
+    try {
         if (c->queue.empty()) c->first_arrival = std::chrono::steady_clock::now();
         c->queue.push_back(&r);
-        c->queued_bytes += len;
-        ++c->n_requests;
-        c->cv_work.notify_one();
-        c->cv_done.wait(lk, [&] { return r.done; });
+    } catch (...) {
+        --c->callers;
+        c->cv_done.notify_all();
+        return CDC_E_NOMEM;
     }
+    c->queued_bytes += len;
+    ++c->n_requests;
+    c->cv_work.notify_all();
+    c->cv_done.wait(lk, [&] { return r.done; });
     *count = r.count;
-    return r.status;
+    const int st = r.status;
+    --c->callers;              // after this, free() may delete c: touch nothing of c below
+    c->cv_done.notify_all();
+    return st;
 }
 
 int cdc_collector_stats(cdc_collector *c, uint64_t *requests, uint64_t *batches)
@@ -167,8 +207,10 @@ int cdc_collector_stats(cdc_collector *c, uint64_t *requests, uint64_t *batches)
     return CDC_OK;
 }
 
-// Drains the queue (pending callers still get their results), then stops the
-// worker.  No call may be made on c afterwards.
+// Stops taking new calls, lets the workers finish every queued call (pending
+// callers still get their results), joins them, and waits until every caller
+// has left cdc_collector_chunk before freeing c.  It may run while callers
+// are blocked in cdc_collector_chunk; no call may START on c once free began.
 void cdc_collector_free(cdc_collector *c)
 {
     if (!c) return;
@@ -177,7 +219,12 @@ void cdc_collector_free(cdc_collector *c)
         c->stop = true;
     }
     c->cv_work.notify_all();
-    if (c->worker.joinable()) c->worker.join();
+    for (auto &t : c->workers)
+        if (t.joinable()) t.join();
+    {
+        std::unique_lock<std::mutex> lk(c->mu);
+        c->cv_done.wait(lk, [&] { return c->callers == 0; });
+    }
     delete c;
 }
 

@@ -743,7 +743,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_enc_plan(const Batch B)
         if (b < B.nblobs) {
             const BlobDesc D = B.blobs[b];
             uint64_t F;
-            if (B.compress) {
+            if (B.compress && D.len == 0) {
+                F = 0;  // DeflateStream of empty input is an empty stream (compression/compression.go:58-62)
+            } else if (B.compress) {
                 uint64_t off = 7;
                 for (uint32_t k = 0; k < D.nblk; ++k) {
                     B.blk_foff[D.blk0 + k] = off;
@@ -954,7 +956,7 @@ __device__ uint32_t xxh32_small(const uint8_t *p, uint32_t n)
 __global__ __launch_bounds__(64) void k_frame_fin(const Batch B)
 {
     const uint32_t b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= B.nblobs || B.status[0]) return;
+    if (b >= B.nblobs || B.status[0] || B.frame_len[b] == 0) return;  // empty blob: no frame at all
     uint8_t *f = frame_ptr(B, b);
     const uint8_t hdr[6] = {0x04, 0x22, 0x4D, 0x18, 0x64, 0x70};
     for (int i = 0; i < 6; ++i) f[i] = hdr[i];
@@ -1548,7 +1550,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
         if (n) {
             ok = hipMemcpyAsync(out_offsets, ws + o_oo, (nb + 1) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
                  hipMemcpyAsync(&status, ws + o_status, 8, hipMemcpyDeviceToHost, s) == hipSuccess;
-        } else {
+        } else if (out_offsets) {
             out_offsets[0] = 0;
         }
         ok = ok && hipStreamSynchronize(s) == hipSuccess;

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "plakar_cdc.h"
 
 namespace cdc {
@@ -122,5 +124,26 @@ struct DigestBatch {
 };
 int launch_digests(const DigestBatch &DB, void *stream);
 extern uint64_t g_digest_lanes;
+
+// cdc_api.cpp: a host-buffer pipeline on one device that outlives one call
+// (the collector's per-device worker).  The source hands out batches of at
+// most kMaxBufsPerLaunch whole buffers; the pipeline stages batch k + 1 into
+// one slot while batch k is chunked in the other, and hands each batch back
+// with its cut lists (and a per-buffer status).
+struct HostBuf {
+    const uint8_t *data;
+    uint64_t len;
+    std::vector<cdc_cut> cuts;
+    int status;
+};
+struct BatchSource {
+    // Fill `batch` and return true, or return false: at once when nothing is
+    // ready and !wait, else only once the source is stopping and empty.
+    virtual bool next(std::vector<HostBuf *> &batch, bool wait) = 0;
+    virtual void finished(std::vector<HostBuf *> &batch) = 0;
+    virtual ~BatchSource() = default;
+};
+int pipeline_device(int dev_index, const cdc_opts *o, BatchSource &src);
+int device_count_initialised();
 
 }  // namespace cdc

@@ -2148,13 +2148,16 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
             n = 256;
         return uint64_t(n);
     }();
-    // Persistent scan (default): one workgroup per CU pulling tasks of 64
-    // lane runs from a counter, about kTasksPerWave tasks per wave, so that
-    // the CUs that run ahead take the tail.
+    // Persistent scan (CDC_SCAN_TASKS_PER_WAVE = k > 0): one workgroup per CU
+    // pulling tasks of 64 lane runs from a counter, about k tasks per wave, so
+    // that the CUs that run ahead take the tail.  Measured slower than the
+    // static grid at every k (2: -3 %, 3: -4 %, 6: -12 % on the driver's
+    // command; shorter lanes add lead bytes and a pipeline fill per task), so
+    // the default is the static grid (0).
     static const uint64_t persist_tpw = [] {
-        const char *e = getenv("CDC_SCAN_TASKS_PER_WAVE");  // 0: static grid (one task per wave)
-        const long v = e ? atol(e) : 3;
-        return uint64_t(v >= 0 && v <= 64 ? v : 3);
+        const char *e = getenv("CDC_SCAN_TASKS_PER_WAVE");
+        const long v = e ? atol(e) : 0;
+        return uint64_t(v >= 0 && v <= 64 ? v : 0);
     }();
     uint64_t wgs = persist_tpw ? cus : (cus > 16 ? cus - 7 : cus);
     if (const char *env = getenv("CDC_SCAN_WGS")) {

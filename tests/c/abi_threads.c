@@ -21,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "plakar_cdc.h"
@@ -253,6 +254,62 @@ static int test_collector(void)
     return bad;
 }
 
+/* ---- 5. collector freed while its callers are still blocked ---------------- */
+static void *collector_one(void *arg)
+{
+    job *j = arg;
+    const uint64_t n = ((uint64_t)(j->id % 3 + 1) << 20) + (uint64_t)j->id * 7919u;
+    uint8_t *p = malloc(n + 1);
+    fill(p, n, 7000 + (uint64_t)j->id);
+    const uint64_t cap = n / g_opts.min_size + 2;
+    cdc_cut *out = malloc(cap * sizeof(cdc_cut));
+    uint64_t cnt = 0, *roff;
+    uint32_t *rlen;
+    const int st = cdc_collector_chunk(g_col, p, n, out, cap, &cnt);
+    const uint64_t nref = ref_cuts(p, n, &roff, &rlen);
+    j->bad |= st != CDC_OK || cnt != nref;
+    for (uint64_t q = 0; q < nref && !j->bad; ++q) j->bad |= out[q].offset != roff[q] || out[q].length != rlen[q];
+    j->chunks = cnt;
+    free(out);
+    free(roff);
+    free(rlen);
+    free(p);
+    return NULL;
+}
+
+static int test_collector_free_while_blocked(void)
+{
+    enum { kCallers = 6 };
+    /* batches close only at 1 GiB, 32 files or after 3 s: the callers stay
+     * blocked until cdc_collector_free closes the batch */
+    if (cdc_collector_new(&g_opts, 1ull << 30, 3000000u, &g_col) != CDC_OK) return 1;
+    pthread_t th[kCallers];
+    job jobs[kCallers];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < kCallers; ++t) {
+        jobs[t] = (job){t, 0, 0};
+        pthread_create(&th[t], NULL, collector_one, &jobs[t]);
+    }
+    uint64_t req = 0, batches = 0;
+    for (int spin = 0; spin < 2000 && req < kCallers; ++spin) {  /* every caller queued (<= 2 s) */
+        usleep(1000);
+        cdc_collector_stats(g_col, &req, &batches);
+    }
+    cdc_collector_free(g_col); /* callers still blocked: free drains them, then waits until they left */
+    g_col = NULL;
+    int bad = req != kCallers;
+    for (int t = 0; t < kCallers; ++t) {
+        pthread_join(th[t], NULL);
+        bad |= jobs[t].bad;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    const double el = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    bad |= el > 2.9; /* free closed the batch instead of waiting out max_wait */
+    printf("collector freed with %d blocked callers: %.2f s, %s\n", kCallers, el, bad ? "MISMATCH" : "identical");
+    return bad;
+}
+
 /* ---- 3. pinned file arena -------------------------------------------------- */
 static int test_files(void)
 {
@@ -327,6 +384,7 @@ int main(void)
     bad |= test_threads();
     bad |= test_files();
     bad |= test_collector();
+    bad |= test_collector_free_while_blocked();
     /* re-init with the same device set is accepted; another set is refused */
     bad |= cdc_init(0, NULL, 0, 0, 0) != CDC_OK;
     bad |= cdc_init(1u << 31, NULL, 0, 0, 0) != CDC_E_NO_DEVICE && cdc_device_count() < 32;

@@ -145,4 +145,6 @@ def decode(data, key=None, compressed=True):
     """(*Repository).Decode of one blob: decrypt, then inflate."""
     if key is not None:
         data, _, _ = decrypt_stream(key, data)
+    if compressed and len(data) == 0:  # InflateStream of empty input (compression/compression.go InflateStream)
+        return b""
     return lz4f_decompress(data) if compressed else data

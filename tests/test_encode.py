@@ -105,6 +105,9 @@ def test_lz4_frames_decode_with_liblz4(kind):
     blobs = _blobs(kind)
     outs = encode.encode_blobs(blobs, key=None, compress=True)
     for b, o in zip(blobs, outs):
+        if not b:  # an empty blob compresses to an empty stream, not a frame (compression/compression.go:58-62)
+            assert o == b""
+            continue
         assert o[:4] == struct.pack("<I", 0x184D2204) and o[4] == 0x64 and o[5] == 0x70
         assert o[6] == (xxhash.xxh32(o[4:6]).intdigest() >> 8) & 0xFF
         assert o[-4:] == struct.pack("<I", xxhash.xxh32(b).intdigest())
@@ -115,6 +118,30 @@ def test_lz4_frames_decode_with_liblz4(kind):
         assert total_out <= total_in + 19 * len(blobs) + 4 * 5  # stored blocks
     else:
         assert total_out < 0.5 * total_in, (total_out, total_in)
+
+
+def test_encode_empty_blob_like_the_reference():
+    """plakar PutBlobs an empty chunk for every empty file
+    (snapshot/backup.go:631-635).  Encode of it: DeflateStream returns an
+    empty stream for empty input (compression/compression.go:58-62), and
+    EncryptStream of an empty stream writes only its 60-byte header -- the
+    subkey nonce and the sealed subkey -- and no piece
+    (encryption/symmetric.go:116-157: ReadFull returns n = 0 at once)."""
+    rnd = os.urandom(56)
+    for compress in (True, False):
+        (enc,) = encode.encode_blobs([b""], key=KEY, compress=compress, random=rnd)
+        assert len(enc) == 60
+        assert enc[:12] == rnd[32:44]
+        assert ref.gcm_open(KEY, enc[:12], enc[12:60]) == rnd[:32]  # the sealed subkey
+        assert ref.decode(enc, key=KEY, compressed=compress) == b""
+        (plain,) = encode.encode_blobs([b""], key=None, compress=compress)
+        assert plain == b""
+    # empty blobs between non-empty ones keep every offset right
+    blobs = [b"", random_bytes(70_000, 3).tobytes(), b"", b"x", b""]
+    outs = encode.encode_blobs(blobs, key=KEY)
+    assert [len(o) for o in outs][0::2] == [60, 60, 60]
+    for b, o in zip(blobs, outs):
+        assert ref.decode(o, key=KEY) == b
 
 
 @pytest.mark.parametrize("compress", [True, False])

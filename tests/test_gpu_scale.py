@@ -168,6 +168,42 @@ def test_file_batch_pinned_arena(oracle, tmp_path):
     fb.close()
 
 
+def test_file_batch_more_files_than_fd_limit(oracle, tmp_path):
+    """A batch of more files than RLIMIT_NOFILE allows: the library holds at
+    most one descriptor per reader thread (stat for sizes, then open / read /
+    close per file), so both file-arena calls succeed with the soft limit
+    lowered to 64 descriptors."""
+    import resource
+    _lib.ensure_init()
+    nfiles = 300
+    sizes = [(i * 7919) % 200_000 + (70_000 if i % 3 == 0 else 0) for i in range(nfiles)]
+    paths, datas = [], []
+    for i, n in enumerate(sizes):
+        a = random_bytes(n, 900 + i)
+        p = tmp_path / f"h{i}"
+        p.write_bytes(a.tobytes())
+        paths.append(str(p))
+        datas.append(a)
+    cap = sum((n + 4095) // 4096 * 4096 for n in sizes)
+    fb = chunkers.FileBatch(cap)
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    resource.setrlimit(resource.RLIMIT_NOFILE, (min(64, hard), hard))
+    try:
+        got_sizes = fb.add_files(paths, threads=8)
+        res1 = fb.chunk(OPTS)
+        fb.reset()
+        res2 = fb.add_and_chunk(paths, OPTS, threads=8)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+    assert got_sizes == sizes
+    gear = _lib.default_gear()
+    for i, a in enumerate(datas):
+        ref = oracle.chunk(a, gear, **DEF)
+        assert_same(res1[i], ref, f"add_files file {i}")
+        assert_same(res2[i], ref, f"chunk_files file {i}")
+    fb.close()
+
+
 def test_file_batch_chunk_files_overlapped(oracle, tmp_path):
     """cdc_batch_chunk_files: the files read into the arena by reader threads
     while the device chunks each >= 256-MiB sub-batch (here two) as soon as

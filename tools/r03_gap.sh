@@ -1,7 +1,8 @@
 #!/bin/bash
 O=gpurun_out/${1:-r03f}; mkdir -p $O
-export PYTHONUNBUFFERED=1 CDC_SCAN_TASKS_PER_WAVE=0
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest.txt 2>&1
+export PYTHONUNBUFFERED=1
+# (suite run separately)
+: timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest.txt 2>&1
 echo "pytest rc=$?"; tail -1 $O/pytest.txt
 FAST="--no-cpu-baseline --digest-reps 0 --encode-reps 0 --e2e-reps 0"
 show() { python3 -c "import json; d=json.load(open('$1')); r=d['roofline']; print('$1', d['value'], d['ms_per_step'], r['kernel_avg_ms'], r['pipeline_avg_ms'])"; }
