@@ -492,6 +492,12 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         sys.exit(2)
+    cdc_env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("CDC_")}
+    diag = [k for k, v in cdc_env.items() if k.startswith("CDC_DIAG") or (k == "CDC_DEBUG_PHASE" and v not in ("", "0"))]
+    if diag:
+        print(f"bench.py: refusing to measure with diagnostic settings {diag} (they change what the kernels do)",
+              file=sys.stderr)
+        sys.exit(2)
     if os.environ.get("BENCH_CPU_SELFTEST") == "1":
         return cpu_selftest(args, world, rank)
 
@@ -665,7 +671,8 @@ def main():
                   "gear": "placeholder (v0.0.8 table unavailable; see DESIGN.md)",
                   "parallelism": f"independent buffers, 1 rank per GPU x {world}, no collective",
                   "per_rank_gibs": [round(per_rank_bytes * args.steps / e / GIB, 2) for e in per_rank],
-                  "chunks_per_step": nchunks}
+                  "chunks_per_step": nchunks,
+                  "cdc_env": cdc_env}
         if host_mode:
             config["routed_bytes_per_gpu"] = routed_bytes
             config["timing"] = ("end-to-end incl. file reads into pinned memory, host->device copies and cut lists back "

@@ -2283,19 +2283,16 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     } else {
         hipLaunchKernelGGL(k_scan, sgrid, sblock, 0, st, B, P, W);
     }
-    // diagnostic (CDC_DIAG_SCAN_ONLY=1): the scan alone, no resolution (cut lists not written)
-    static const bool scan_only = [] {
-        const char *e = getenv("CDC_DIAG_SCAN_ONLY");
-        return e && e[0] == '1';
-    }();
-    if (scan_only) {
-        if (prof) {
-            std::lock_guard<std::mutex> lk(g_prof_mu);
-            (void)hipEventRecord(pr.e2, st);
-            g_prof_live.push_back(pr);
-        }
-        return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+#ifdef CDC_DIAG_SCAN_ONLY
+    // build-time diagnostic only (-DCDC_DIAG_SCAN_ONLY, never in the shipped
+    // library): the scan alone, no resolution, cut lists not written
+    if (prof) {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        (void)hipEventRecord(pr.e2, st);
+        g_prof_live.push_back(pr);
     }
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+#endif
     // MaskL index of the tasks near long MaskS-free stretches (most workgroups
     // exit after one look at the MaskS index on ordinary data)
     if (B.total_tasks > 0 && B.maskl_index && !fused)
@@ -2385,6 +2382,3 @@ extern "C" int cdc_profile_collect(double *scan_ms, double *pipeline_ms, uint64_
     return st;
 }
 
-namespace cdc {
-
-}  // namespace cdc

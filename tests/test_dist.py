@@ -97,3 +97,13 @@ def test_bench_refuses_a_mismatched_launcher():
     rc, line, err = _run_bench(["--gpus", "2"], {"BENCH_CPU_SELFTEST": "1", "WORLD_SIZE": "1", "RANK": "0"})
     assert rc != 0 and line is None
     assert "WORLD_SIZE=1" in err
+
+
+def test_bench_refuses_diagnostic_settings():
+    """bench.py will not measure with settings that change what the kernels do
+    (CDC_DIAG_*, a non-zero CDC_DEBUG_PHASE); every CDC_* variable it accepts
+    is recorded in the line's config."""
+    rc, line, err = _run_bench(["--gpus", "1"], {"BENCH_CPU_SELFTEST": "1", "CDC_DEBUG_PHASE": "16"})
+    assert rc == 2 and line is None and "CDC_DEBUG_PHASE" in err
+    rc, line, err = _run_bench(["--gpus", "1"], {"BENCH_CPU_SELFTEST": "1", "CDC_DIAG_ANYTHING": "1"})
+    assert rc == 2 and "CDC_DIAG_ANYTHING" in err

@@ -67,7 +67,7 @@ def main():
     # last kernel end among the timed passes (the two streams interleave, so take the max)
     t_end = max(e for s, e, n in ks[starts[a.warmup]:last])
     span = (t_end - t_first) / 1e3
-    print(f"\ntimed region on the device: {span:.1f} us for {a.steps} passes = {span / a.steps:.4f} ms/pass")
+    print(f"\ntimed region on the device: {span:.1f} us for {a.steps} passes = {span / a.steps:.1f} us/pass")
     for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         print(f"  {k:16s} n={len(v):4d} avg={sum(v) / len(v):8.2f} min={min(v):8.2f} max={max(v):8.2f}")
     # bench.py's roofline loop: the next max(5, min(K, 50)) passes, one stream,
