@@ -43,6 +43,11 @@ WORKLOADS = {
                      "library (pread, 16 threads) into its pinned arena and chunked (pinned H2D, cut lists to host), "
                      "the reads running ahead of the device by 256-MiB sub-batches; warm page cache",
                 nbuf=512, size=0, kind="zipf", host=True, files=True),
+    "c4b": dict(desc="C4 end-to-end backup: the same 512-file share written to disk once (untimed), then per step "
+                     "the whole backup through the native pipeline (cdc_backup_run): reads + object SHA-256, cut "
+                     "points, chunk SHA-256 + histograms, BlobExists, Encode (LZ4 + AES-256-GCM, random key), 8 "
+                     "concurrent packers -> packfiles (20 MiB); every file, small ones included; warm page cache",
+                nbuf=512, size=0, kind="zipf", host=True, files=True, backup=True),
 }
 
 
@@ -532,6 +537,7 @@ def main():
     L = _lib.lib()
 
     routed_bytes = 0
+    post_step = None  # turns the last step's output into cut rows, after the timed region
     if host_mode:
         corpus = make_host_corpus(wl, rank, world)
         # plakar chunkify routing (snapshot/backup.go:631-644): files < MinSize are one chunk, no CDC
@@ -543,6 +549,12 @@ def main():
         def step():
             return chunkers.ChunkBuffers(host_bufs, opts)
 
+        backup_stats = [None]
+        if wl.get("backup"):  # every file of the share, small ones included: the pipeline routes them
+            host_bufs = corpus
+            routed_bytes = 0
+            per_rank_bytes = sum(a.size for a in host_bufs)
+            nbufs = len(host_bufs)
         if wl.get("files"):
             import tempfile
             tmpdir = tempfile.mkdtemp(prefix="cdc_c4f_")
@@ -558,6 +570,25 @@ def main():
             def step():
                 fbatch.reset()
                 return fbatch.add_and_chunk(paths, opts, threads=16)
+
+            if wl.get("backup"):
+                from plakar_amd import snapshot
+                session = snapshot.BackupSession(key=os.urandom(32), compression="LZ4", packers=8, readers=16,
+                                                 dev=local)
+
+                def step():  # one whole backup of the share per step (an empty repository each time)
+                    objs, _, st = session.run(paths, keep_packfiles=False)
+                    backup_stats[0] = st
+                    return objs
+
+                def post_step(objs):  # after the timed region: the (offset, length) rows, as the chunker reports them
+                    import numpy as np
+                    out = []  # (none for an empty file)
+                    for o in objs:
+                        lens = np.array([c.Length for c in o.Chunks if c.Length], dtype=np.uint64)
+                        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if lens.size else lens
+                        out.append(np.stack([offs, lens], axis=1) if lens.size else np.zeros((0, 2), np.uint64))
+                    return out
     else:
         size = (args.size_mib << 20) if args.size_mib else wl["size"]
         bufs = make_buffers(torch, wl, rank, dev, size, world)
@@ -584,6 +615,8 @@ def main():
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
+    if post_step is not None:
+        out = post_step(out)
     elapsed = reduce_max(dist, world, t1 - t0, dev)
     per_rank = gather_per_rank(dist, world, t1 - t0, dev)
     value = world * per_rank_bytes * args.steps / elapsed / GIB
@@ -699,6 +732,13 @@ def main():
             "chunk_digests": digest,
             "encode": encode_res,
         }
+        if host_mode and wl.get("backup") and backup_stats[0]:
+            bs = backup_stats[0]
+            line["backup_stages"] = dict(
+                {k: (round(v, 4) if isinstance(v, float) else v) for k, v in bs.items()},
+                note="per step (the last one): seconds per stage; read_s / pack_s / objhash_s are thread times "
+                     "summed over batches or threads, device_s the calling thread's device stages; the stages "
+                     "overlap (reads of batch k+1 and packing of batch k run during batch k's device work)")
         print(json.dumps(line), flush=True)
     if host_mode and wl.get("files"):
         import shutil

@@ -195,6 +195,80 @@ int cdc_packer_serialize_part(const cdc_packer *p, int part, int64_t timestamp, 
 void cdc_packer_reset(cdc_packer *p);
 void cdc_packer_free(cdc_packer *p);
 
+/* ---- end-to-end backup: files in, packfiles out ---------------------------------
+ * chunkify (snapshot/backup.go:571-687) + PutBlob (snapshot/blobs.go:9-24) +
+ * packerJob (snapshot/snapshot.go:51-92) for a list of files, as a pipeline
+ * over batches of whole files (at most batch_bytes each, 0: 256 MiB): reader
+ * threads read each file into a pinned arena and SHA-256 it there (the
+ * object checksum); the device cuts, digests (SHA-256 + byte histogram per
+ * chunk) and Encodes the new chunks (LZ4 when compress, then AES-256-GCM
+ * when key != NULL; a chunk whose digest is in `known` (sorted, 32 B each:
+ * BlobExists) or was already seen in this run is not stored again); packer
+ * threads append the blobs to their own packfiles and hand each one, at
+ * Size() > packfile_max (0: 20 MiB) and at the end, to on_pack (PutPackfile;
+ * calls are serialised, from packer threads).  on_file is called once per
+ * file, in order, from one library thread (the calling thread meanwhile
+ * drives the next batches through the device), with pointers valid during the
+ * call only; chunk entropies come from the device (cdc_chunk_entropy_device_async).
+ * An empty file is one empty chunk (backup.go:631-635); a file shorter than
+ * MinSize is one chunk.  Returns the first failure (CDC_E_IO for a file that
+ * cannot be read, a negative status from on_pack). */
+typedef struct cdc_backup_opts {
+    cdc_opts chunking;
+    uint32_t packfile_max;
+    int compress;
+    const uint8_t *key;       /* 32-byte repository key, or NULL: no encryption */
+    int packers;              /* packer threads (0: 8, NumCPU in the reference) */
+    int readers;              /* reader threads (0: 8) */
+    uint64_t batch_bytes;
+    const uint8_t *known;     /* sorted digests already in the repository, or NULL */
+    uint64_t nknown;
+    int64_t timestamp;        /* packfile footer timestamp */
+} cdc_backup_opts;
+typedef struct cdc_backup_file {
+    int index;                /* position in paths */
+    int status;
+    uint8_t checksum[32];     /* SHA-256 of the whole file (Object.Checksum) */
+    uint64_t size;
+    uint64_t nchunks;
+    const cdc_cut *cuts;      /* (offset, length) in the file */
+    const uint8_t *digests;   /* 32 B per chunk (Chunk.Checksum) */
+    const uint32_t *hists;    /* 256 per chunk (entropy / Distribution) */
+    const uint8_t *is_new;    /* 1: stored by this run (PutBlob), 0: deduplicated */
+    const double *entropy;    /* per chunk (Chunk.Entropy: entropy() with Go's math.Log2) */
+    double object_entropy;    /* Object.Entropy: sum of entropy * length in chunk order / size */
+} cdc_backup_file;
+typedef struct cdc_backup_stats {
+    uint64_t files, bytes, chunks, new_blobs, new_bytes, encoded_bytes, packfiles, packed_bytes, batches;
+    double read_s;            /* file reads, summed over reader threads */
+    double objhash_s;         /* object SHA-256, summed over reader threads */
+    double h2d_s, chunk_s, digest_s, d2h_s, encode_s;  /* device stages (events; Encode: host wall) */
+    double device_s;          /* the calling thread's time in the device stages (callbacks excluded) */
+    double callback_s;        /* in on_file (the callback thread) */
+    double pack_s;            /* packer threads' busy time, summed */
+    double wall_s;
+} cdc_backup_stats;
+typedef void (*cdc_backup_file_fn)(void *ctx, const cdc_backup_file *f);
+typedef int (*cdc_backup_pack_fn)(void *ctx, const uint8_t *packfile, uint64_t len);
+/* A backup context: its options (key and known digests copied), streams and
+ * pinned / device buffers kept across calls (grown on demand).  Each
+ * cdc_backup_files call is one backup of the given files: its dedup set
+ * starts empty (plus `known`).  One call at a time per context. */
+typedef struct cdc_backup cdc_backup;
+int cdc_backup_new(int device, const cdc_backup_opts *opts, cdc_backup **out);
+int cdc_backup_files(cdc_backup *b, const char *const *paths, int n, cdc_backup_file_fn on_file,
+                     cdc_backup_pack_fn on_pack, void *ctx, cdc_backup_stats *stats);
+void cdc_backup_free(cdc_backup *b);
+/* new + files + free in one call. */
+int cdc_backup_run(int device, const char *const *paths, int n, const cdc_backup_opts *opts,
+                   cdc_backup_file_fn on_file, cdc_backup_pack_fn on_pack, void *ctx, cdc_backup_stats *stats);
+
+/* The library's host SHA-256 (x86 SHA extensions when the CPU has them;
+ * force_scalar != 0 takes the portable path).  cdc_sha256_accelerated: 1 if
+ * the SHA extensions are in use. */
+int cdc_sha256(const void *data, uint64_t len, int force_scalar, uint8_t out[32]);
+int cdc_sha256_accelerated(void);
+
 /* ---- pinned batch arena: files in, host cut lists out --------------------------
  * Replaces the importer's per-file os.Open + bufio reads
  * (snapshot/importer/fs/fs.go:69-71) feeding the per-file Next() loop: a
@@ -278,6 +352,13 @@ int cdc_chunk_digests_device_batch_async(int device, const void *const *d_data, 
                                          const cdc_cut *const *d_cuts, const uint64_t *cut_caps,
                                          const cdc_result *const *d_results, uint8_t *const *d_digests,
                                          uint32_t *const *d_hist, void *stream);
+/* entropy() of snapshot/backup.go:548-569 for `rows` histogram rows (256
+ * uint32 each, as cdc_chunk_digests* writes them; a row's sum is its chunk's
+ * length) into d_entropy (float64 per row): the reference's terms with Go's
+ * math.Log2, one IEEE operation at a time, summed in bin order (bit-exact);
+ * 0 for an all-zero row.  Asynchronous on `stream`. */
+int cdc_chunk_entropy_device_async(int device, const uint32_t *d_hist, uint64_t rows, double *d_entropy,
+                                   void *stream);
 
 /* ---- streaming chunker: chunkers.NewChunker / (*Chunker).Next -----------------
  * Push model, so cgo never hands a Go pointer to asynchronous HIP work: the

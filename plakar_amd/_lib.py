@@ -49,6 +49,31 @@ class cdc_result(ctypes.Structure):
                 ("status", ctypes.c_int64), ("needed", ctypes.c_uint64)]
 
 
+class cdc_backup_opts(ctypes.Structure):
+    _fields_ = [("chunking", cdc_opts), ("packfile_max", ctypes.c_uint32), ("compress", ctypes.c_int),
+                ("key", ctypes.c_void_p), ("packers", ctypes.c_int), ("readers", ctypes.c_int),
+                ("batch_bytes", ctypes.c_uint64), ("known", ctypes.c_void_p), ("nknown", ctypes.c_uint64),
+                ("timestamp", ctypes.c_int64)]
+
+
+class cdc_backup_file(ctypes.Structure):
+    _fields_ = [("index", ctypes.c_int), ("status", ctypes.c_int), ("checksum", ctypes.c_uint8 * 32),
+                ("size", ctypes.c_uint64), ("nchunks", ctypes.c_uint64), ("cuts", ctypes.POINTER(cdc_cut)),
+                ("digests", ctypes.POINTER(ctypes.c_uint8)), ("hists", ctypes.POINTER(ctypes.c_uint32)),
+                ("is_new", ctypes.POINTER(ctypes.c_uint8)), ("entropy", ctypes.POINTER(ctypes.c_double)),
+                ("object_entropy", ctypes.c_double)]
+
+
+class cdc_backup_stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("files", "bytes", "chunks", "new_blobs", "new_bytes", "encoded_bytes",
+                                               "packfiles", "packed_bytes", "batches")] + \
+               [(n, ctypes.c_double) for n in ("read_s", "objhash_s", "h2d_s", "chunk_s", "digest_s", "d2h_s",
+                                               "encode_s", "device_s", "callback_s", "pack_s", "wall_s")]
+
+
+BACKUP_FILE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(cdc_backup_file))
+BACKUP_PACK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint64)
+
 CUT_DTYPE_FIELDS = [("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")]
 READ_FN = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64)
 
@@ -142,6 +167,16 @@ SIGNATURES = {
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_set_walk_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_backup_run": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_char_p), ctypes.c_int, _P(cdc_backup_opts),
+                                      BACKUP_FILE_FN, BACKUP_PACK_FN, ctypes.c_void_p, _P(cdc_backup_stats)]),
+    "cdc_backup_new": (ctypes.c_int, [ctypes.c_int, _P(cdc_backup_opts), _P(ctypes.c_void_p)]),
+    "cdc_backup_files": (ctypes.c_int, [ctypes.c_void_p, _P(ctypes.c_char_p), ctypes.c_int, BACKUP_FILE_FN,
+                                        BACKUP_PACK_FN, ctypes.c_void_p, _P(cdc_backup_stats)]),
+    "cdc_backup_free": (None, [ctypes.c_void_p]),
+    "cdc_sha256": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, _P(ctypes.c_uint8)]),
+    "cdc_sha256_accelerated": (ctypes.c_int, []),
+    "cdc_chunk_entropy_device_async": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                      ctypes.c_void_p]),
     "cdc_debug_maskl_state": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_uint32), _P(ctypes.c_uint64)]),
     "cdc_debug_set_digest_lanes": (ctypes.c_int, [ctypes.c_uint64]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),

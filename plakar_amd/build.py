@@ -16,7 +16,7 @@ LIB_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIB_DIR, "libplakar_cdc.so")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("cdc_kernels.hip", "cdc_digest.hip", "cdc_api.cpp",
                                                     "cdc_packer.cpp", "cdc_collector.cpp",
-                                                    "cdc_encode.hip")]
+                                                    "cdc_encode.hip", "cdc_sha256.cpp", "cdc_backup.cpp")]
 HEADERS = [os.path.join(HERE, "csrc", "cdc_internal.h"), os.path.join(ROOT, "include", "plakar_cdc.h")]
 ARCH = os.environ.get("PLAKAR_CDC_ARCH", "gfx950")
 

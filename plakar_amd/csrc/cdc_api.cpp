@@ -1036,6 +1036,16 @@ int cdc_chunk_digests_device_async(int device, const void *d_data, uint64_t len,
                                                 d_hist ? &d_hist : nullptr, stream);
 }
 
+int cdc_chunk_entropy_device_async(int device, const uint32_t *d_hist, uint64_t rows, double *d_entropy, void *stream)
+{
+    if (rows && (!d_hist || !d_entropy)) return CDC_E_INVALID;
+    DeviceCtx *ctx = nullptr;
+    int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    return launch_entropy(d_hist, rows, d_entropy, stream);
+}
+
 int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out, uint64_t out_cap,
               uint64_t *out_counts, uint64_t *out_needed)
 {

@@ -1,0 +1,910 @@
+// End-to-end backup pipeline: files in, packfiles out (SURVEY.md section 8f
+// rank 3, the consumer side of the chunker).
+//
+// The reference runs, per file and in one goroutine per file
+// (snapshot/backup.go:216-225), chunkify (backup.go:571-687): the importer's
+// reads (snapshot/importer/fs/fs.go:69-71), the chunker's Next() loop
+// (backup.go:647-665), per chunk processChunk (backup.go:594-629: SHA-256,
+// byte histogram -> entropy, BlobExists, PutBlob), the object's SHA-256 over
+// the whole file; PutBlob (snapshot/blobs.go:9-24) Encodes each new chunk
+// (repository/repository.go:212-236: LZ4 then AES-256-GCM) and hands it to
+// NumCPU packerJob workers (snapshot/snapshot.go:51-92), each appending to its
+// own packfile and flushing it at Size() > MaxSize.
+//
+// Here the same work runs as a pipeline over batches of whole files, built on
+// the library's own entry points:
+//   reader threads   pread each file of batch k into a pinned arena slot and
+//                    hash it there (the object checksum, host SHA-256 with the
+//                    CPU's SHA extensions: one serial chain per file)
+//   device (caller)  H2D, cut points (cdc_chunk_device_batch_async), per-chunk
+//                    SHA-256 + histograms (cdc_chunk_digests_device_batch_async),
+//                    D2H of the lists; host dedup (the run's own set + the
+//                    caller's known digests: BlobExists); Encode of the new
+//                    chunks in device memory (cdc_encode_device); D2H of the
+//                    encoded blobs; per-file callback (the Object's fields)
+//   packer threads   Packer.AddBlob into their own packfile (cdc_packer_*),
+//                    flush at Size() > MaxSize to the packfile callback
+//                    (PutPackfile)
+// Four slots (arena + device buffers) rotate, so later batches are read while
+// batch k is on the device and earlier ones are packed; the per-file
+// callbacks run on their own thread while the device takes the next batches.
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/random.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <unordered_set>
+#include <vector>
+
+#include "cdc_internal.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+struct Digest {
+    uint8_t b[32];
+    bool operator==(const Digest &o) const { return std::memcmp(b, o.b, 32) == 0; }
+};
+struct DigestHash {
+    size_t operator()(const Digest &d) const
+    {
+        size_t h;
+        std::memcpy(&h, d.b, sizeof(h));  // SHA-256 output: any 8 bytes are uniform
+        return h;
+    }
+};
+
+int read_exact(const char *path, uint8_t *dst, uint64_t len)
+{
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return CDC_E_IO;
+    uint64_t got = 0;
+    int st = CDC_OK;
+    while (got < len) {
+        const ssize_t k = pread(fd, dst + got, size_t(std::min<uint64_t>(len - got, 1ull << 30)), off_t(got));
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) {
+            st = CDC_E_IO;
+            break;
+        }
+        got += uint64_t(k);
+    }
+    close(fd);
+    return st;
+}
+
+struct Batch {
+    uint32_t f0, f1;      // files [f0, f1)
+    uint64_t bytes;       // arena bytes (files 256-B aligned)
+    uint64_t cuts_cap;    // sum of len / Min + 2
+};
+
+// Buffers of one pipeline slot.  Kept by the context across runs and grown
+// on demand (pinned allocations are slow: they are made once per session).
+struct Slot {
+    uint8_t *h_arena = nullptr, *d_in = nullptr;
+    uint64_t arena_cap = 0;
+    void *d_ws = nullptr;
+    uint64_t ws_cap = 0;
+    cdc_cut *d_cuts = nullptr, *h_cuts = nullptr, *d_acuts = nullptr;  // file-relative; arena-relative
+    uint64_t *h_meta = nullptr, *d_meta = nullptr;                        // (cut0, cap, arena_off) per file
+    cdc_result *d_res = nullptr, *h_res = nullptr;
+    uint8_t *d_dig = nullptr, *h_dig = nullptr;
+    uint32_t *d_hist = nullptr, *h_hist = nullptr;
+    double *d_ent = nullptr, *h_ent = nullptr;
+    uint64_t cuts_cap = 0, res_cap = 0;
+    uint8_t *d_enc = nullptr, *h_enc = nullptr;
+    uint64_t enc_cap = 0, henc_cap = 0;
+    // A: H2D start / end, cut points end; D: digests start / end, lists back
+    hipEvent_t ev[6] = {};
+    // per run: lifecycle (guarded by Run::mu) and the enqueued batch's lists
+    int batch = -1, next = 0;  // the batch in the slot; the one that takes it next
+    bool read_done = false, hash_done = false, device_done = false;
+    uint32_t nread = 0, nhashed = 0;
+    uint64_t pending = 0;  // blobs not yet packed
+    std::vector<uint64_t> lens, cut0;
+    uint64_t ncut = 0;
+    double t_enq = 0;
+    std::vector<uint8_t> is_new;       // per chunk of the batch (BlobExists' answer)
+    std::vector<uint64_t> file_new0;   // per file: its first entry in is_new
+};
+
+// Four slots: batches k + 1 .. k + 3 are read (and object-hashed: a 128-MiB
+// file is one ~64-ms SHA-256 chain on a host core) while batch k is on the
+// device and batch k - 1 is packed; with two, reads and packing serialise,
+// with three a large file's hash stalls the readers.
+constexpr int kSlots = 4;
+constexpr int kA = 0, kD = 1, kE = 2;  // cdc_backup::stream
+
+#define HIPOK(x)                                         \
+    do {                                                 \
+        if ((x) != hipSuccess) return CDC_E_DEVICE;      \
+    } while (0)
+
+template <typename T>
+int grow_dev(T *&p, uint64_t &cap, uint64_t need)
+{
+    if (need <= cap && p) return CDC_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIPOK(hipMalloc(reinterpret_cast<void **>(&p), need ? need : 1));
+    cap = need;
+    return CDC_OK;
+}
+
+template <typename T>
+int grow_host(T *&p, uint64_t need, uint64_t have)
+{
+    if (need <= have && p) return CDC_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    HIPOK(hipHostMalloc(reinterpret_cast<void **>(&p), need ? need : 1, hipHostMallocDefault));
+    return CDC_OK;
+}
+
+int grow_slot(Slot &s, uint64_t arena, uint64_t ws, uint64_t ncuts, uint64_t nfiles)
+{
+    int st;
+    if (!s.ev[0])
+        for (auto &e : s.ev) HIPOK(hipEventCreate(&e));
+    if (arena > s.arena_cap || !s.h_arena) {
+        if ((st = grow_host(s.h_arena, arena, 0)) != CDC_OK) return st;
+        uint64_t c = s.arena_cap;
+        if ((st = grow_dev(s.d_in, c, arena)) != CDC_OK) return st;
+        s.arena_cap = arena;
+    }
+    if ((st = grow_dev(s.d_ws, s.ws_cap, std::max<uint64_t>(ws, 256))) != CDC_OK) return st;
+    if (ncuts > s.cuts_cap || !s.h_cuts) {
+        uint64_t c = s.cuts_cap * sizeof(cdc_cut);
+        if ((st = grow_dev(s.d_cuts, c, ncuts * sizeof(cdc_cut))) != CDC_OK) return st;
+        if ((st = grow_host(s.h_cuts, ncuts * sizeof(cdc_cut), 0)) != CDC_OK) return st;
+        c = s.cuts_cap * sizeof(cdc_cut);
+        if ((st = grow_dev(s.d_acuts, c, ncuts * sizeof(cdc_cut))) != CDC_OK) return st;
+        c = s.cuts_cap * 32;
+        if ((st = grow_dev(s.d_dig, c, ncuts * 32)) != CDC_OK) return st;
+        if ((st = grow_host(s.h_dig, ncuts * 32, 0)) != CDC_OK) return st;
+        c = s.cuts_cap * 1024;
+        if ((st = grow_dev(s.d_hist, c, ncuts * 1024)) != CDC_OK) return st;
+        if ((st = grow_host(s.h_hist, ncuts * 1024, 0)) != CDC_OK) return st;
+        c = s.cuts_cap * 8;
+        if ((st = grow_dev(s.d_ent, c, ncuts * 8)) != CDC_OK) return st;
+        if ((st = grow_host(s.h_ent, ncuts * 8, 0)) != CDC_OK) return st;
+        s.cuts_cap = ncuts;
+    }
+    if (nfiles > s.res_cap || !s.h_res) {
+        uint64_t c = s.res_cap * sizeof(cdc_result);
+        if ((st = grow_dev(s.d_res, c, nfiles * sizeof(cdc_result))) != CDC_OK) return st;
+        if ((st = grow_host(s.h_res, nfiles * sizeof(cdc_result), 0)) != CDC_OK) return st;
+        c = s.res_cap * 24;
+        if ((st = grow_dev(s.d_meta, c, nfiles * 24)) != CDC_OK) return st;
+        if ((st = grow_host(s.h_meta, nfiles * 24, 0)) != CDC_OK) return st;
+        s.res_cap = nfiles;
+    }
+    return CDC_OK;
+}
+
+void free_slot(Slot &s)
+{
+    for (void *p : {static_cast<void *>(s.d_in), s.d_ws, static_cast<void *>(s.d_cuts), static_cast<void *>(s.d_res),
+                    static_cast<void *>(s.d_acuts), static_cast<void *>(s.d_meta),
+                    static_cast<void *>(s.d_dig), static_cast<void *>(s.d_hist), static_cast<void *>(s.d_ent),
+                    static_cast<void *>(s.d_enc)})
+        if (p) (void)hipFree(p);
+    for (void *p : {static_cast<void *>(s.h_arena), static_cast<void *>(s.h_cuts), static_cast<void *>(s.h_res),
+                    static_cast<void *>(s.h_meta),
+                    static_cast<void *>(s.h_dig), static_cast<void *>(s.h_hist), static_cast<void *>(s.h_ent),
+                    static_cast<void *>(s.h_enc)})
+        if (p) (void)hipHostFree(p);
+    for (auto &e : s.ev)
+        if (e) (void)hipEventDestroy(e);
+    s = Slot();
+}
+
+}  // namespace
+
+struct cdc_backup {
+    int device = 0;
+    cdc_backup_opts o;
+    std::vector<uint8_t> key;    // the repository key, copied (o.key points here)
+    std::vector<uint8_t> known;  // sorted digests, copied (o.known points here)
+    Slot slot[kSlots];
+    std::vector<cdc_packer *> packers;  // kept across runs (their buffers stay reserved and mapped)
+    // A: H2D + cut points (ahead); D: digests, entropy, lists; E: Encode and
+    // the encoded blobs back (beside the next batch's digests on D)
+    hipStream_t stream[3] = {nullptr, nullptr, nullptr};
+};
+
+namespace {
+
+struct Blob {
+    Digest sum;
+    const uint8_t *data;
+    uint64_t len;
+    int slot;
+};
+
+struct Run {
+    cdc_backup *B;
+    const cdc_backup_opts &o;
+    const char *const *paths;
+    int n;
+    cdc_backup_file_fn on_file;
+    cdc_backup_pack_fn on_pack;
+    void *ctx;
+    std::vector<uint64_t> size, arena_off;
+    std::vector<Batch> batches;
+    std::vector<uint32_t> batch_of;  // per file
+    std::atomic<uint32_t> next_file{0};
+    std::vector<Digest> obj;  // per file
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<int> status{CDC_OK};
+    bool stop_packers = false;
+    size_t devices_done = 0;  // batches through finish_device (callbacks may start)
+    std::deque<Blob> queue;
+    std::mutex sink_mu;
+    std::unordered_set<Digest, DigestHash> seen;
+    cdc_backup_stats st{};
+    std::mutex stat_mu;
+
+    Run(cdc_backup *b, const char *const *p, int nn) : B(b), o(b->o), paths(p), n(nn) {}
+
+    void fail(int s)
+    {
+        int ok = CDC_OK;
+        status.compare_exchange_strong(ok, s);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+        }
+        cv.notify_all();
+    }
+};
+
+int plan(Run &R, uint64_t &arena_cap, uint64_t &cuts_cap, uint64_t &ws_cap, uint64_t &files_cap)
+{
+    const uint64_t bb = R.o.batch_bytes ? R.o.batch_bytes : (256ull << 20);
+    R.size.resize(size_t(R.n));
+    R.arena_off.resize(size_t(R.n));
+    R.obj.resize(size_t(R.n));
+    R.batch_of.resize(size_t(R.n));
+    Batch cur{0, 0, 0, 0};
+    for (int i = 0; i < R.n; ++i) {
+        struct stat sb;
+        if (!R.paths[i] || stat(R.paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) return CDC_E_IO;
+        const uint64_t len = uint64_t(sb.st_size);
+        const uint64_t need = (len + 255) & ~255ull;
+        if (cur.f1 > cur.f0 && (cur.bytes + need > bb || cur.f1 - cur.f0 >= 4096)) {
+            R.batches.push_back(cur);
+            cur = Batch{uint32_t(i), uint32_t(i), 0, 0};
+        }
+        R.size[size_t(i)] = len;
+        R.batch_of[size_t(i)] = uint32_t(R.batches.size());
+        R.arena_off[size_t(i)] = cur.bytes;
+        cur.bytes += need;
+        cur.cuts_cap += len / R.o.chunking.min_size + 2;
+        cur.f1 = uint32_t(i + 1);
+    }
+    if (cur.f1 > cur.f0) R.batches.push_back(cur);
+    arena_cap = cuts_cap = ws_cap = files_cap = 0;
+    for (const Batch &b : R.batches) {
+        arena_cap = std::max(arena_cap, std::max<uint64_t>(b.bytes, 256));
+        cuts_cap = std::max(cuts_cap, b.cuts_cap);
+        files_cap = std::max<uint64_t>(files_cap, b.f1 - b.f0);
+        for (uint32_t g = b.f0; g < b.f1; g += cdc::kMaxBufsPerLaunch) {
+            const uint32_t e = std::min<uint32_t>(b.f1, g + cdc::kMaxBufsPerLaunch);
+            uint64_t ws = 0;
+            const int s = cdc_device_batch_workspace_size(R.size.data() + g, int(e - g), &R.o.chunking, &ws);
+            if (s != CDC_OK) return s;
+            ws_cap = std::max(ws_cap, ws);
+        }
+    }
+    return CDC_OK;
+}
+
+// A slot is free once its batch left the device, every blob of it is packed
+// and every file of it hashed.  Called with R.mu held.
+void maybe_release(Run &R, Slot &s)
+{
+    if (s.device_done && s.hash_done && s.pending == 0 && s.batch >= 0) {
+        s.batch = -1;
+        R.cv.notify_all();
+    }
+}
+
+// Reader threads: file after file in batch order (a slot is claimed by the
+// first file of its batch once the batch three back released it), each file
+// read into the slot's arena and then hashed there (the object checksum, one
+// serial chain: a large file's hash no longer holds back the batch's reads or
+// the next batch; it gates only the callbacks and the slot's release).
+void reader_main(Run &R)
+{
+    double read_s = 0, hash_s = 0;
+    for (uint32_t i; (i = R.next_file.fetch_add(1)) < uint32_t(R.n) && R.status.load() == CDC_OK;) {
+        const uint32_t k = R.batch_of[i];
+        const Batch &b = R.batches[k];
+        Slot &s = R.B->slot[k % kSlots];
+        {
+            std::unique_lock<std::mutex> lk(R.mu);
+            R.cv.wait(lk, [&] {
+                return R.status.load() != CDC_OK || s.batch == int(k) || (s.batch < 0 && s.next == int(k));
+            });
+            if (R.status.load() != CDC_OK) break;
+            if (s.batch != int(k)) {
+                s.batch = int(k);
+                s.next = int(k) + kSlots;
+                s.read_done = s.hash_done = s.device_done = false;
+                s.nread = s.nhashed = 0;
+                s.pending = 0;
+            }
+        }
+        uint8_t *dst = s.h_arena + R.arena_off[i];
+        const auto t0 = Clock::now();
+        const int st = read_exact(R.paths[i], dst, R.size[i]);
+        const auto t1 = Clock::now();
+        read_s += secs(t0, t1);
+        if (st != CDC_OK) {
+            R.fail(st);
+            break;
+        }
+        bool wake;
+        {
+            std::lock_guard<std::mutex> lk(R.mu);
+            wake = ++s.nread == b.f1 - b.f0;
+            s.read_done = s.read_done || wake;
+        }
+        if (wake) R.cv.notify_all();
+        cdc::sha256(dst, R.size[i], R.obj[i].b);
+        hash_s += secs(t1, Clock::now());
+        {
+            std::lock_guard<std::mutex> lk(R.mu);
+            wake = ++s.nhashed == b.f1 - b.f0;
+            if (wake) {
+                s.hash_done = true;
+                maybe_release(R, s);
+            }
+        }
+        if (wake) R.cv.notify_all();
+    }
+    std::lock_guard<std::mutex> lk(R.stat_mu);
+    R.st.read_s += read_s;
+    R.st.objhash_s += hash_s;
+}
+
+// The packer's packfile, serialized in place, to PutPackfile (on_pack).
+int sink(Run &R, cdc_packer *p)
+{
+    const uint8_t *data = nullptr;
+    uint64_t len = 0;
+    const int st = cdc::packer_seal(p, R.o.timestamp, &data, &len);
+    if (st != CDC_OK) return st;
+    std::lock_guard<std::mutex> lk(R.sink_mu);
+    ++R.st.packfiles;
+    R.st.packed_bytes += len;
+    return R.on_pack ? R.on_pack(R.ctx, data, len) : CDC_OK;
+}
+
+void packer_main(Run &R, cdc_packer *p)
+{
+    cdc_packer_reset(p);
+    double busy = 0;
+    for (;;) {
+        Blob b;
+        {
+            std::unique_lock<std::mutex> lk(R.mu);
+            R.cv.wait(lk, [&] { return !R.queue.empty() || R.stop_packers || R.status.load() != CDC_OK; });
+            if (R.queue.empty()) break;
+            b = R.queue.front();
+            R.queue.pop_front();
+        }
+        const auto t0 = Clock::now();
+        int st = R.status.load() == CDC_OK ? cdc_packer_add_blob(p, 1 /* TYPE_CHUNK */, b.sum.b, b.data, b.len) : 0;
+        if (st == 1) {  // Size() > MaxSize: packerJob flushes (snapshot/snapshot.go:71)
+            st = sink(R, p);
+            cdc_packer_reset(p);
+        }
+        busy += secs(t0, Clock::now());
+        if (st < 0) R.fail(st);
+        {
+            std::lock_guard<std::mutex> lk(R.mu);
+            Slot &s = R.B->slot[b.slot];
+            --s.pending;
+            maybe_release(R, s);
+        }
+    }
+    const auto t0 = Clock::now();
+    if (R.status.load() == CDC_OK && cdc_packer_count(p)) {  // the last, partial packfile
+        const int st = sink(R, p);
+        if (st < 0) R.fail(st);
+    }
+    busy += secs(t0, Clock::now());
+    cdc_packer_reset(p);
+    std::lock_guard<std::mutex> lk(R.stat_mu);
+    R.st.pack_s += busy;
+}
+
+int random_bytes(uint8_t *p, size_t n)
+{
+    while (n) {
+        const ssize_t k = getrandom(p, n, 0);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return CDC_E_IO;
+        p += k;
+        n -= size_t(k);
+    }
+    return CDC_OK;
+}
+
+// Object.Entropy (snapshot/backup.go:612-627, 668-670): totalEntropy +=
+// entropy * float64(len) over the chunks in order, then / float64(size); one
+// IEEE operation at a time.
+#pragma clang fp contract(off)
+double object_entropy(const double *e, const cdc_cut *cuts, uint64_t n, uint64_t size)
+{
+    double acc = 0.0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const double t = e[i] * double(cuts[i].length);
+        acc = i ? acc + t : t;
+    }
+    return size ? acc / double(size) : 0.0;
+}
+#pragma clang fp contract(on)
+
+const uint8_t kEmptySum[32] = {0xe3, 0xb0, 0xc4, 0x42, 0x98, 0xfc, 0x1c, 0x14, 0x9a, 0xfb, 0xf4,
+                               0xc8, 0x99, 0x6f, 0xb9, 0x24, 0x27, 0xae, 0x41, 0xe4, 0x64, 0x9b,
+                               0x93, 0x4c, 0xa4, 0x95, 0x99, 0x1b, 0x78, 0x52, 0xb8, 0x55};  // SHA-256("")
+
+// Stage A on stream 1, enqueued as soon as the batch's bytes are in its slot
+// (it runs beside the previous batch's digests and Encode: the copy engine
+// and a short scan): H2D, cut points of every non-empty file (a file < Min is
+// one chunk, as chunkify routes it: the Algorithm returns n for n <= Min).
+int enqueue_cuts(Run &R, size_t k)
+{
+    Slot &s = R.B->slot[k % kSlots];
+    const Batch &b = R.batches[k];
+    const cdc_opts *co = &R.o.chunking;
+    const uint32_t nf = b.f1 - b.f0;
+    hipStream_t st1 = R.B->stream[kA];
+    const auto w0 = Clock::now();
+    HIPOK(hipEventRecord(s.ev[0], st1));
+    HIPOK(hipMemcpyAsync(s.d_in, s.h_arena, b.bytes, hipMemcpyHostToDevice, st1));
+    HIPOK(hipEventRecord(s.ev[1], st1));
+    std::vector<const void *> dp(nf);
+    std::vector<uint64_t> caps(nf);
+    std::vector<cdc_cut *> cp(nf);
+    std::vector<cdc_result *> rp(nf);
+    s.lens.assign(nf, 0);
+    s.cut0.assign(nf, 0);
+    uint64_t c = 0;
+    for (uint32_t j = 0; j < nf; ++j) {
+        const uint32_t i = b.f0 + j;
+        dp[j] = s.d_in + R.arena_off[i];
+        s.lens[j] = R.size[i];
+        caps[j] = R.size[i] / co->min_size + 2;
+        s.cut0[j] = c;
+        cp[j] = s.d_cuts + c;
+        rp[j] = s.d_res + j;
+        c += caps[j];
+    }
+    s.ncut = c;
+    for (uint32_t g = 0; g < nf; g += cdc::kMaxBufsPerLaunch) {
+        const int m = int(std::min<uint32_t>(cdc::kMaxBufsPerLaunch, nf - g));
+        const int st = cdc_chunk_device_batch_async(R.B->device, dp.data() + g, s.lens.data() + g, m, 1, co,
+                                                    cp.data() + g, caps.data() + g, rp.data() + g, s.d_ws, s.ws_cap,
+                                                    st1);
+        if (st != CDC_OK) return st;
+    }
+    HIPOK(hipEventRecord(s.ev[2], st1));
+    s.t_enq = secs(w0, Clock::now());
+    return CDC_OK;
+}
+
+// Stage B on stream D (after stage A): the batch's cut lists rewritten as
+// one arena-relative list (k_arena_cuts), one digest launch group for every
+// chunk of every file (SHA-256 + histograms), entropy per chunk, the lists
+// back to pinned memory.  Batch k + 1's stage B is enqueued before batch k's
+// Encode (stream E), so the device's digest chains run back to back.
+int enqueue_digests(Run &R, size_t k)
+{
+    Slot &s = R.B->slot[k % kSlots];
+    const Batch &b = R.batches[k];
+    const uint32_t nf = b.f1 - b.f0;
+    hipStream_t sd = R.B->stream[kD];
+    const auto w0 = Clock::now();
+    HIPOK(hipStreamWaitEvent(sd, s.ev[2], 0));
+    for (uint32_t j = 0; j < nf; ++j) {
+        s.h_meta[3 * j] = s.cut0[j];
+        s.h_meta[3 * j + 1] = s.lens[j] / R.o.chunking.min_size + 2;
+        s.h_meta[3 * j + 2] = R.arena_off[b.f0 + j];
+    }
+    const uint64_t c = s.ncut;
+    HIPOK(hipEventRecord(s.ev[3], sd));
+    HIPOK(hipMemcpyAsync(s.d_meta, s.h_meta, 24ull * nf, hipMemcpyHostToDevice, sd));
+    int st = cdc::launch_arena_cuts(s.d_meta, nf, s.d_res, s.d_cuts, s.d_acuts, sd);
+    if (st != CDC_OK) return st;
+    st = cdc_chunk_digests_device_async(R.B->device, s.d_in, b.bytes, s.d_acuts, c, nullptr, s.d_dig, s.d_hist, sd);
+    if (st != CDC_OK) return st;
+    if ((st = cdc_chunk_entropy_device_async(R.B->device, s.d_hist, c, s.d_ent, sd)) != CDC_OK) return st;
+    HIPOK(hipEventRecord(s.ev[4], sd));
+    HIPOK(hipMemcpyAsync(s.h_res, s.d_res, nf * sizeof(cdc_result), hipMemcpyDeviceToHost, sd));
+    HIPOK(hipMemcpyAsync(s.h_cuts, s.d_cuts, c * sizeof(cdc_cut), hipMemcpyDeviceToHost, sd));
+    HIPOK(hipMemcpyAsync(s.h_dig, s.d_dig, c * 32, hipMemcpyDeviceToHost, sd));
+    HIPOK(hipMemcpyAsync(s.h_hist, s.d_hist, c * 1024, hipMemcpyDeviceToHost, sd));
+    HIPOK(hipMemcpyAsync(s.h_ent, s.d_ent, c * 8, hipMemcpyDeviceToHost, sd));
+    HIPOK(hipEventRecord(s.ev[5], sd));
+    s.t_enq += secs(w0, Clock::now());
+    return CDC_OK;
+}
+
+// Batch k once its lists are back: dedup (BlobExists: the run's own chunks and
+// the caller's known digests), Encode of the new chunks on stream E, the
+// encoded blobs back, the blobs to the packers.
+int finish_device(Run &R, size_t k)
+{
+    Slot &s = R.B->slot[k % kSlots];
+    const Batch &b = R.batches[k];
+    const uint32_t nf = b.f1 - b.f0;
+    const auto w0 = Clock::now();
+    HIPOK(hipEventSynchronize(s.ev[5]));
+    float t[4] = {};  // H2D, cut points, digests + entropy, lists back
+    HIPOK(hipEventElapsedTime(&t[0], s.ev[0], s.ev[1]));
+    HIPOK(hipEventElapsedTime(&t[1], s.ev[1], s.ev[2]));
+    HIPOK(hipEventElapsedTime(&t[2], s.ev[3], s.ev[4]));
+    HIPOK(hipEventElapsedTime(&t[3], s.ev[4], s.ev[5]));
+    const Digest *kn = reinterpret_cast<const Digest *>(R.o.known);
+    auto known = [&](const Digest &d) {
+        return R.o.nknown && std::binary_search(kn, kn + R.o.nknown, d, [](const Digest &a, const Digest &x) {
+                   return std::memcmp(a.b, x.b, 32) < 0;
+               });
+    };
+    std::vector<uint64_t> enc_off, enc_len;
+    std::vector<Digest> enc_sum;
+    std::vector<uint8_t> &is_new = s.is_new;
+    std::vector<uint64_t> &file_new0 = s.file_new0;
+    is_new.clear();
+    file_new0.assign(nf, 0);
+    uint64_t enc_bound = 0, nchunks = 0, new_bytes = 0;
+    for (uint32_t j = 0; j < nf; ++j) {
+        const cdc_result &r = s.h_res[j];
+        if (s.lens[j] && r.status != CDC_OK) return int(r.status);
+        file_new0[j] = is_new.size();
+        const uint64_t cn = s.lens[j] ? r.ncuts : 1;  // an empty file is one empty chunk (backup.go:631-635)
+        for (uint64_t q = 0; q < cn; ++q) {
+            Digest d;
+            uint64_t off = 0, len = 0;
+            if (s.lens[j]) {
+                const cdc_cut &cc = s.h_cuts[s.cut0[j] + q];
+                std::memcpy(d.b, s.h_dig + 32 * (s.cut0[j] + q), 32);
+                off = R.arena_off[b.f0 + j] + cc.offset;
+                len = cc.length;
+            } else {
+                std::memcpy(d.b, kEmptySum, 32);
+            }
+            const bool fresh = !known(d) && R.seen.insert(d).second;
+            is_new.push_back(fresh ? 1 : 0);
+            if (fresh) {
+                enc_off.push_back(off);
+                enc_len.push_back(len);
+                enc_sum.push_back(d);
+                enc_bound += cdc_encode_bound(len, R.o.compress, R.o.key != nullptr);
+                new_bytes += len;
+            }
+        }
+        nchunks += cn;
+    }
+    const uint32_t nb = uint32_t(enc_off.size());
+    const bool encode = nb && (R.o.compress || R.o.key);
+    std::vector<uint64_t> oo(nb + 1, 0);
+    double enc_s = 0, d2h_enc_s = 0;
+    int st;
+    if (encode) {
+        if ((st = grow_dev(s.d_enc, s.enc_cap, enc_bound)) != CDC_OK) return st;
+        std::vector<uint8_t> rnd;
+        if (R.o.key) {
+            rnd.resize(56ull * nb);
+            if ((st = random_bytes(rnd.data(), rnd.size())) != CDC_OK) return st;
+        }
+        const auto e0 = Clock::now();
+        st = cdc_encode_device(R.B->device, s.d_in, enc_off.data(), enc_len.data(), nb, R.o.compress, R.o.key,
+                               R.o.key ? rnd.data() : nullptr, s.d_enc, s.enc_cap, oo.data(), R.B->stream[kE]);
+        if (st != CDC_OK) return st;
+        const auto e1 = Clock::now();
+        if (oo[nb] > s.henc_cap || !s.h_enc) {
+            const uint64_t want = std::max<uint64_t>(oo[nb], s.enc_cap);
+            if ((st = grow_host(s.h_enc, want, 0)) != CDC_OK) return st;
+            s.henc_cap = want;
+        }
+        HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, R.B->stream[kE]));
+        HIPOK(hipStreamSynchronize(R.B->stream[kE]));
+        enc_s = secs(e0, e1);
+        d2h_enc_s = secs(e1, Clock::now());
+    }
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        for (uint32_t q = 0; q < nb; ++q) {
+            const uint8_t *p = encode ? s.h_enc + oo[q] : s.h_arena + enc_off[q];
+            const uint64_t len = encode ? oo[q + 1] - oo[q] : enc_len[q];
+            R.queue.push_back(Blob{enc_sum[q], p, len, int(k % kSlots)});
+        }
+        s.pending += nb;
+    }
+    R.cv.notify_all();
+    std::lock_guard<std::mutex> lk(R.stat_mu);
+    R.st.batches += 1;
+    R.st.files += nf;
+    for (uint32_t j = 0; j < nf; ++j) R.st.bytes += s.lens[j];
+    R.st.chunks += nchunks;
+    R.st.new_blobs += nb;
+    R.st.new_bytes += new_bytes;
+    R.st.encoded_bytes += encode ? oo[nb] : new_bytes;
+    R.st.h2d_s += t[0] * 1e-3;
+    R.st.chunk_s += t[1] * 1e-3;
+    R.st.digest_s += t[2] * 1e-3;
+    R.st.d2h_s += t[3] * 1e-3 + d2h_enc_s;
+    R.st.encode_s += enc_s;
+    R.st.device_s += s.t_enq + secs(w0, Clock::now());
+    return CDC_OK;
+}
+
+// Batch k's per-file callbacks (the Object's fields), on the callback thread
+// while the calling thread drives the next batches through the device; the
+// slot is released once its blobs are packed too.
+int finish_host(Run &R, size_t k)
+{
+    Slot &s = R.B->slot[k % kSlots];
+    const Batch &b = R.batches[k];
+    const uint32_t nf = b.f1 - b.f0;
+    {
+        std::unique_lock<std::mutex> lk(R.mu);  // the batch's lists + dedup, and every object checksum
+        R.cv.wait(lk, [&] { return (R.devices_done > k && s.hash_done) || R.status.load() != CDC_OK; });
+    }
+    if (R.status.load() != CDC_OK) return R.status.load();
+    const auto cb0 = Clock::now();
+    if (R.on_file) {
+        static const cdc_cut kEmptyCut = {0, 0, 0};
+        static const uint32_t kZeroHist[256] = {};
+        static const double kZeroEnt[1] = {0.0};
+        for (uint32_t j = 0; j < nf; ++j) {
+            cdc_backup_file f;
+            std::memset(&f, 0, sizeof(f));
+            f.index = int(b.f0 + j);
+            f.status = CDC_OK;
+            std::memcpy(f.checksum, R.obj[b.f0 + j].b, 32);
+            f.size = s.lens[j];
+            const bool empty = s.lens[j] == 0;
+            f.nchunks = empty ? 1 : s.h_res[j].ncuts;
+            f.cuts = empty ? &kEmptyCut : s.h_cuts + s.cut0[j];
+            f.digests = empty ? kEmptySum : s.h_dig + 32 * s.cut0[j];
+            f.hists = empty ? kZeroHist : s.h_hist + 256 * s.cut0[j];
+            f.is_new = s.is_new.data() + s.file_new0[j];
+            f.entropy = empty ? kZeroEnt : s.h_ent + s.cut0[j];
+            f.object_entropy = empty ? 0.0 : object_entropy(f.entropy, f.cuts, f.nchunks, f.size);
+            R.on_file(R.ctx, &f);
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        s.device_done = true;
+        maybe_release(R, s);
+    }
+    R.cv.notify_all();
+    std::lock_guard<std::mutex> lk(R.stat_mu);
+    R.st.callback_s += secs(cb0, Clock::now());
+    return CDC_OK;
+}
+
+void callback_main(Run &R)
+{
+    for (size_t k = 0; k < R.batches.size(); ++k) {
+        const int st = finish_host(R, k);
+        if (st != CDC_OK) {
+            R.fail(st);
+            return;
+        }
+    }
+}
+
+// Wait until batch k's bytes are in its slot (the reader's signal).
+int wait_read(Run &R, size_t k)
+{
+    Slot &s = R.B->slot[k % kSlots];
+    std::unique_lock<std::mutex> lk(R.mu);
+    R.cv.wait(lk, [&] { return (s.batch == int(k) && s.read_done) || R.status.load() != CDC_OK; });
+    return R.status.load();
+}
+
+bool read_ready(Run &R, size_t k)
+{
+    Slot &s = R.B->slot[k % kSlots];
+    std::lock_guard<std::mutex> lk(R.mu);
+    return s.batch == int(k) && s.read_done;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdc_backup_new(int device, const cdc_backup_opts *opts, cdc_backup **out)
+{
+    if (!opts || !out) return CDC_E_INVALID;
+    *out = nullptr;
+    int st = cdc_validate("fastcdc", &opts->chunking);
+    if (st != CDC_OK) return st;
+    if (opts->nknown && !opts->known) return CDC_E_INVALID;
+    if (!cdc::device_count_initialised()) return CDC_E_NOT_INIT;
+    auto *b = new (std::nothrow) cdc_backup();
+    if (!b) return CDC_E_NOMEM;
+    try {
+        b->device = device;
+        b->o = *opts;
+        if (opts->key) {
+            b->key.assign(opts->key, opts->key + 32);
+            b->o.key = b->key.data();
+        }
+        if (opts->nknown) {
+            b->known.assign(opts->known, opts->known + 32 * opts->nknown);
+            b->o.known = b->known.data();
+        }
+    } catch (...) {
+        delete b;
+        return CDC_E_NOMEM;
+    }
+    bool ok = hipSetDevice(device) == hipSuccess;
+    for (auto &sm : b->stream) ok = ok && hipStreamCreateWithFlags(&sm, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
+        cdc_backup_free(b);
+        return CDC_E_DEVICE;
+    }
+    *out = b;
+    return CDC_OK;
+}
+
+int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_file_fn on_file,
+                     cdc_backup_pack_fn on_pack, void *ctx, cdc_backup_stats *stats)
+{
+    if (!B || n < 0 || (n && !paths)) return CDC_E_INVALID;
+    const auto w0 = Clock::now();
+    Run *Rp = new (std::nothrow) Run(B, paths, n);
+    if (!Rp) return CDC_E_NOMEM;
+    Run &R = *Rp;
+    R.on_file = on_file;
+    R.on_pack = on_pack;
+    R.ctx = ctx;
+    int st = CDC_OK;
+    std::vector<std::thread> readers, packers;
+    std::thread callbacks;
+    try {
+        uint64_t arena = 0, ncuts = 0, ws = 0, nfiles = 0;
+        st = plan(R, arena, ncuts, ws, nfiles);
+        if (st == CDC_OK && hipSetDevice(B->device) != hipSuccess) st = CDC_E_DEVICE;
+        for (int i = 0; i < kSlots && st == CDC_OK && !R.batches.empty(); ++i) {
+            st = grow_slot(B->slot[i], arena, ws, ncuts, nfiles);
+            B->slot[i].batch = -1;
+            B->slot[i].next = i;
+            B->slot[i].read_done = B->slot[i].hash_done = B->slot[i].device_done = false;
+            B->slot[i].pending = 0;
+        }
+        if (st == CDC_OK && !R.batches.empty()) {
+            const int np = std::max(1, R.o.packers ? R.o.packers : 8);
+            while (int(B->packers.size()) < np) {
+                cdc_packer *p = nullptr;
+                if (cdc_packer_new(R.o.packfile_max ? R.o.packfile_max : (20u << 20), &p) != CDC_OK) {
+                    st = CDC_E_NOMEM;
+                    break;
+                }
+                B->packers.push_back(p);
+                cdc::packer_reserve(p, cdc_encode_bound(R.o.chunking.max_size, R.o.compress, R.o.key != nullptr));
+            }
+            if (st != CDC_OK) throw std::bad_alloc();
+            const int nr = std::max(1, R.o.readers ? R.o.readers : 8);
+            for (int r = 0; r < nr; ++r) readers.emplace_back([&R] { reader_main(R); });
+            callbacks = std::thread([&R] { callback_main(R); });
+            for (int p = 0; p < np; ++p) {
+                cdc_packer *pk = B->packers[size_t(p)];
+                packers.emplace_back([&R, pk] { packer_main(R, pk); });
+            }
+            // Per batch k: stage A (H2D, cut points) of every later batch
+            // whose bytes are in (slots permitting), stage B (digests) of
+            // batch k + 1 when its stage A is enqueued, then batch k is
+            // deduplicated, Encoded and handed to the packers and the
+            // callback thread.  Nothing here waits for a read unless the
+            // device would otherwise idle.
+            const size_t nb = R.batches.size();
+            size_t cuts = 0, digs = 0;  // batches whose stage A / stage B is enqueued
+            for (size_t k = 0; k < nb && st == CDC_OK; ++k) {
+                if (digs == k) {
+                    if (cuts == k) {
+                        if ((st = wait_read(R, k)) != CDC_OK || (st = enqueue_cuts(R, k)) != CDC_OK) break;
+                        ++cuts;
+                    }
+                    if ((st = enqueue_digests(R, k)) != CDC_OK) break;
+                    ++digs;
+                }
+                while (cuts < nb && cuts < k + kSlots && read_ready(R, cuts)) {
+                    if ((st = enqueue_cuts(R, cuts)) != CDC_OK) break;
+                    ++cuts;
+                }
+                if (st != CDC_OK) break;
+                if (digs == k + 1 && cuts > k + 1) {
+                    if ((st = enqueue_digests(R, k + 1)) != CDC_OK) break;
+                    ++digs;
+                }
+                if ((st = finish_device(R, k)) != CDC_OK) break;
+                {
+                    std::lock_guard<std::mutex> lk(R.mu);
+                    R.devices_done = k + 1;
+                }
+                R.cv.notify_all();
+            }
+            if (st == CDC_OK && callbacks.joinable()) {
+                callbacks.join();  // the last slots are released by the callbacks
+                st = R.status.load();
+            }
+            if (st != CDC_OK) R.fail(st);
+            {
+                std::lock_guard<std::mutex> lk(R.mu);
+                R.stop_packers = true;
+            }
+            R.cv.notify_all();
+        }
+    } catch (const std::bad_alloc &) {
+        st = CDC_E_NOMEM;
+        R.fail(st);
+    } catch (...) {
+        st = CDC_E_DEVICE;
+        R.fail(st);
+    }
+    if (callbacks.joinable()) callbacks.join();
+    for (auto &t : readers) t.join();
+    for (auto &t : packers) t.join();
+    if (st == CDC_OK) st = R.status.load();
+    if (st != CDC_OK) {  // leave the context reusable: nothing of this run in flight
+        for (auto &sm : B->stream) (void)hipStreamSynchronize(sm);
+    }
+    R.st.wall_s = secs(w0, Clock::now());
+    if (stats) *stats = R.st;
+    delete Rp;
+    return st;
+}
+
+void cdc_backup_free(cdc_backup *b)
+{
+    if (!b) return;
+    for (auto &s : b->stream)
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    for (auto &s : b->slot) free_slot(s);
+    for (cdc_packer *p : b->packers) cdc_packer_free(p);
+    delete b;
+}
+
+int cdc_backup_run(int device, const char *const *paths, int n, const cdc_backup_opts *opts,
+                   cdc_backup_file_fn on_file, cdc_backup_pack_fn on_pack, void *ctx, cdc_backup_stats *stats)
+{
+    cdc_backup *b = nullptr;
+    int st = cdc_backup_new(device, opts, &b);
+    if (st != CDC_OK) return st;
+    st = cdc_backup_files(b, paths, n, on_file, on_pack, ctx, stats);
+    cdc_backup_free(b);
+    return st;
+}
+
+}  // extern "C"

@@ -452,6 +452,121 @@ __global__ __launch_bounds__(kHistWaves * 64) void k_chunk_hist(const DigestBatc
     }
 }
 
+// entropy() of snapshot/backup.go:548-569 from a byte histogram row: e = 0;
+// for b in 0..255 with f_b > 0: p = f_b / len; e -= p * Log2(p), with Go's
+// math.Log2 (math/log2.go: Frexp, frac == 0.5 -> exp - 1, else
+// Log(frac) * (1/Ln2) + exp) and Go's Log (math/log.go, the fdlibm e_log.c
+// reduction and polynomial).  Every step is one IEEE double operation in the
+// reference's order: contraction into FMAs is off for this code, division is
+// the correctly rounded lowering.  Restated from plakar_amd/hashing.py
+// go_log2 / entropy_from_freq, whose parity tests pin it.
+#pragma clang fp contract(off)
+__device__ __forceinline__ double go_log2_dev(double x)
+{
+    // x = p in (0, 1]: a normal double (p >= 2^-64), so Frexp is the exponent field
+    const uint64_t bits = uint64_t(__double_as_longlong(x));
+    const int e2 = int((bits >> 52) & 0x7FFu) - 1022;
+    double frac = __longlong_as_double(int64_t((bits & 0x800FFFFFFFFFFFFFull) | (1022ull << 52)));
+    if (frac == 0.5) return double(e2 - 1);
+    // Log(frac): frac = f1 * 2^0, f1 in [0.5, 1)
+    double f1 = frac;
+    int ki = 0;
+    if (f1 < 0.70710678118654757) {  // math.Sqrt2 / 2 (rounded)
+        f1 *= 2.0;
+        ki = -1;
+    }
+    const double f = f1 - 1.0;
+    const double k = double(ki);
+    const double s = f / (2.0 + f);
+    const double s2 = s * s;
+    const double s4 = s2 * s2;
+    const double t1 = s2 * (6.666666666666735130e-01 + s4 * (2.857142874366239149e-01 +
+                                                           s4 * (1.818357216161805012e-01 + s4 * 1.479819860511658591e-01)));
+    const double t2 = s4 * (3.999999999940941908e-01 + s4 * (2.222219843214978396e-01 + s4 * 1.531383769920937332e-01));
+    const double r = t1 + t2;
+    const double hfsq = 0.5 * f * f;
+    const double lg = k * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + r) + k * 1.90821492927058770002e-10)) - f);
+    return lg * 1.4426950408889634 + double(e2);  // 0x1.71547652b82fep+0: Go's 1/Ln2
+}
+
+// One wave per histogram row: lane l holds bins 4l .. 4l + 3 (one coalesced
+// KiB per row), computes their terms, and the wave folds them in bin order
+// (the reference's sequential e -= term: a fixed order, so bit-exact).
+constexpr uint32_t kEntWaves = 4;
+__global__ __launch_bounds__(kEntWaves * 64) void k_chunk_entropy(const uint32_t *__restrict__ hist, uint64_t rows,
+                                                                  double *__restrict__ out)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = uint64_t(gridDim.x) * kEntWaves;
+    for (uint64_t r = uint64_t(blockIdx.x) * kEntWaves + (threadIdx.x >> 6); r < rows; r += waves) {
+        const uint4 h = reinterpret_cast<const uint4 *>(hist + r * 256u)[lane];
+        uint64_t len = uint64_t(h.x) + h.y + h.z + h.w;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) len += __shfl_xor(len, o, 64);
+        const double dl = double(len);
+        const uint32_t hv[4] = {h.x, h.y, h.z, h.w};
+        double t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double p = double(hv[j]) / dl;
+            t[j] = hv[j] ? p * go_log2_dev(p) : 0.0;
+        }
+        double e = 0.0;
+        for (int l = 0; l < 64; ++l) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const double tj = __shfl(t[j], l, 64);
+                const uint32_t hj = __shfl(hv[j], l, 64);
+                if (hj) e -= tj;
+            }
+        }
+        if (lane == 0) out[r] = len ? e : 0.0;
+    }
+}
+#pragma clang fp contract(on)
+
+int launch_entropy(const uint32_t *d_hist, uint64_t rows, double *d_out, void *stream)
+{
+    if (!rows) return CDC_OK;
+    const uint64_t wgs = std::min<uint64_t>((rows + kEntWaves - 1) / kEntWaves, 256u * 8u);
+    hipLaunchKernelGGL(k_chunk_entropy, dim3(uint32_t(wgs)), dim3(kEntWaves * 64), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_hist, rows, d_out);
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+}
+
+// A batch of files laid out in one arena (the backup pipeline's slots) as ONE
+// digest buffer: file j's cut list sits at slots [cut0_j, cut0_j + cap_j) of
+// `cuts` with offsets relative to the file; out[slot] is the same cut with
+// the file's arena offset added, or an empty chunk at 0 for the slots past
+// the file's count.  One digest launch then covers every file of the batch
+// (a launch lasts as long as its longest chunk, so one launch per batch, not
+// one per 32 files).  meta: (cut0, cap, arena_off) per file.
+__global__ __launch_bounds__(256) void k_arena_cuts(const uint64_t *__restrict__ meta,
+                                                    const cdc_result *__restrict__ res,
+                                                    const cdc_cut *__restrict__ cuts, cdc_cut *__restrict__ out)
+{
+    const uint32_t j = blockIdx.x;
+    const uint64_t c0 = meta[3 * j], cap = meta[3 * j + 1], base = meta[3 * j + 2];
+    const uint64_t n = min<uint64_t>(cap, res[j].ncuts);
+    for (uint64_t q = threadIdx.x; q < cap; q += blockDim.x) {
+        cdc_cut c = {0, 0, 0};
+        if (q < n) {
+            c = cuts[c0 + q];
+            c.offset += base;
+        }
+        out[c0 + q] = c;
+    }
+}
+
+int launch_arena_cuts(const uint64_t *d_meta, uint32_t nfiles, const cdc_result *d_res, const cdc_cut *d_cuts,
+                      cdc_cut *d_out, void *stream)
+{
+    if (!nfiles) return CDC_OK;
+    hipLaunchKernelGGL(k_arena_cuts, dim3(nfiles), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_meta, d_res,
+                       d_cuts, d_out);
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+}
+
 uint64_t g_digest_lanes = 0;  // cdc_debug_set_digest_lanes (0: from the device's CU count)
 
 int launch_digests(const DigestBatch &DB, void *stream)

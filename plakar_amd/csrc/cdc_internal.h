@@ -123,6 +123,9 @@ struct DigestBatch {
     DigestBuf b[kMaxBufsPerLaunch];
 };
 int launch_digests(const DigestBatch &DB, void *stream);
+int launch_entropy(const uint32_t *d_hist, uint64_t rows, double *d_out, void *stream);
+int launch_arena_cuts(const uint64_t *d_meta, uint32_t nfiles, const cdc_result *d_res, const cdc_cut *d_cuts,
+                      cdc_cut *d_out, void *stream);
 extern uint64_t g_digest_lanes;
 
 // cdc_api.cpp: a host-buffer pipeline on one device that outlives one call
@@ -145,5 +148,24 @@ struct BatchSource {
 };
 int pipeline_device(int dev_index, const cdc_opts *o, BatchSource &src);
 int device_count_initialised();
+
+// cdc_sha256.cpp: host SHA-256 (x86 SHA extensions when present).
+struct Sha256 {
+    uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                     0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+    uint8_t buf[64];
+    uint64_t total = 0;
+    size_t fill = 0;
+    bool force_scalar = false;
+    void blocks(const uint8_t *p, size_t nblocks);
+    void update(const uint8_t *p, size_t n);
+    void final(uint8_t out[32]);
+};
+void sha256(const void *data, size_t n, uint8_t out[32], bool force_scalar = false);
+bool sha256_accelerated();
+
+// cdc_packer.cpp: in-place serialization for the backup pipeline's sinks
+int packer_seal(cdc_packer *p, int64_t timestamp, const uint8_t **data, uint64_t *len);
+void packer_reserve(cdc_packer *p, uint64_t max_blob);
 
 }  // namespace cdc

@@ -20,87 +20,7 @@
 
 namespace {
 
-// ---- SHA-256 (FIPS 180-4), for the index checksum -------------------------
-struct Sha256 {
-    uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                     0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-    uint8_t buf[64];
-    uint64_t total = 0;
-    size_t fill = 0;
-
-    static uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-
-    void block(const uint8_t *p)
-    {
-        static const uint32_t K[64] = {
-            0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
-            0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
-            0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
-            0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
-            0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
-            0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
-            0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
-            0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
-        uint32_t w[64];
-        for (int i = 0; i < 16; ++i)
-            w[i] = uint32_t(p[4 * i]) << 24 | uint32_t(p[4 * i + 1]) << 16 | uint32_t(p[4 * i + 2]) << 8 | p[4 * i + 3];
-        for (int i = 16; i < 64; ++i) {
-            const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
-            const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
-            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-        }
-        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-        for (int i = 0; i < 64; ++i) {
-            const uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + w[i];
-            const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
-            hh = g;
-            g = f;
-            f = e;
-            e = d + t1;
-            d = c;
-            c = b;
-            b = a;
-            a = t1 + t2;
-        }
-        h[0] += a;
-        h[1] += b;
-        h[2] += c;
-        h[3] += d;
-        h[4] += e;
-        h[5] += f;
-        h[6] += g;
-        h[7] += hh;
-    }
-
-    void update(const uint8_t *p, size_t n)
-    {
-        total += n;
-        while (n) {
-            const size_t k = std::min(n, size_t(64) - fill);
-            std::memcpy(buf + fill, p, k);
-            fill += k;
-            p += k;
-            n -= k;
-            if (fill == 64) {
-                block(buf);
-                fill = 0;
-            }
-        }
-    }
-
-    void final(uint8_t out[32])
-    {
-        const uint64_t bits = total * 8;
-        const uint8_t one = 0x80, zero = 0;
-        update(&one, 1);
-        while (fill != 56) update(&zero, 1);
-        uint8_t len[8];
-        for (int i = 0; i < 8; ++i) len[i] = uint8_t(bits >> (56 - 8 * i));
-        update(len, 8);
-        for (int i = 0; i < 8; ++i)
-            for (int j = 0; j < 4; ++j) out[4 * i + j] = uint8_t(h[i] >> (24 - 8 * j));
-    }
-};
+using cdc::Sha256;  // cdc_sha256.cpp
 
 template <typename T>
 void put_le(std::vector<uint8_t> &v, T x)
@@ -224,6 +144,37 @@ int cdc_packer_serialize_part(const cdc_packer *p, int part, int64_t timestamp, 
     if (*len) std::memcpy(out, src, *len);
     return CDC_OK;
 }
+
+}  // extern "C"
+
+namespace cdc {
+
+// Serialize in place for a packfile sink: the index and footer are appended
+// to the data section's own buffer (no copy of the blobs), *data / *len then
+// hold the packfile until cdc_packer_reset.  The buffer is reserved at MaxSize
+// plus one maximal blob so that AddBlob does not reallocate.
+int packer_seal(cdc_packer *p, int64_t timestamp, const uint8_t **data, uint64_t *len)
+{
+    if (!p || !data || !len) return CDC_E_INVALID;
+    std::vector<uint8_t> footer;
+    serialize_footer(p, timestamp, footer);  // IndexOffset = len(Blobs), before the append
+    p->blobs.insert(p->blobs.end(), p->index.begin(), p->index.end());
+    p->blobs.insert(p->blobs.end(), footer.begin(), footer.end());
+    *data = p->blobs.data();
+    *len = p->blobs.size();
+    return CDC_OK;
+}
+
+void packer_reserve(cdc_packer *p, uint64_t max_blob)
+{
+    if (!p) return;
+    p->blobs.reserve(size_t(p->max_size) + size_t(max_blob) + (1u << 20));
+    p->index.reserve(1u << 20);
+}
+
+}  // namespace cdc
+
+extern "C" {
 
 void cdc_packer_reset(cdc_packer *p)
 {

@@ -102,6 +102,22 @@ def chunk_digests_batch(datas, cut_lists, results=None, hist=True, stream=None):
     return outs
 
 
+def chunk_entropy_device(hist, stream=None):
+    """entropy() per histogram row on the device (cdc_chunk_entropy_device_async):
+    hist is a (n, 256) int32/uint32 CUDA tensor as chunk_digests returns it;
+    returns a float64 (n,) CUDA tensor, bit-equal to entropy_rows."""
+    assert hist.is_cuda and hist.dim() == 2 and hist.shape[1] == 256 and hist.element_size() == 4
+    _lib.ensure_init()
+    hist = hist.contiguous()
+    out = torch.empty(hist.shape[0], dtype=torch.float64, device=hist.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(hist.device)
+    check(lib().cdc_chunk_entropy_device_async(hist.device.index, ctypes.c_void_p(hist.data_ptr()), hist.shape[0],
+                                               ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream.cuda_stream)),
+          "entropy")
+    return out
+
+
 # --------------------------------------------------------------------- Go Log2
 # fdlibm e_log.c constants (Go math/log.go uses the same algorithm)
 _LN2_HI = 6.93147180369123816490e-01

@@ -232,4 +232,120 @@ def backup_batch(files, repo: Repository = None, known=None, max_size=None, enco
     return objects, packs
 
 
-__all__ = ["Object", "route", "chunkify_batch", "backup_batch"]
+class BackupSession:
+    """A native backup context (cdc_backup_new): the repository's chunking
+    parameters, Encode configuration (compression "LZ4" or None, the 32-byte
+    key or None), the digests already stored (BlobExists), packfile MaxSize
+    and the worker counts, with its device buffers kept across runs.  Each
+    run() is one backup of a list of files through the pipeline of
+    cdc_backup_files (reads + object SHA-256, cut points, chunk SHA-256 +
+    histograms, dedup, Encode, `packers` concurrent packerJob workers,
+    snapshot/snapshot.go:51-92)."""
+
+    def __init__(self, repo: Repository = None, key=None, compression="LZ4", known=None, max_size=None,
+                 packers=8, readers=8, batch_bytes=256 << 20, timestamp=0, dev=0):
+        import ctypes
+        from . import _lib, packer as packer_mod
+        repo = repo or Repository()
+        cfg = repo.Chunking
+        opts = chunkers.ChunkerOpts(MinSize=int(cfg.MinSize), NormalSize=int(cfg.NormalSize),
+                                    MaxSize=int(cfg.MaxSize))
+        chunkers.Validate(cfg.Algorithm.lower(), opts)
+        if compression not in (None, "LZ4"):
+            raise ValueError(f"unsupported compression {compression!r}")
+        _lib.ensure_init()
+        o = _lib.cdc_backup_opts()
+        o.chunking = _lib.cdc_opts(opts.MinSize, opts.NormalSize, opts.MaxSize, 0)
+        o.packfile_max = int(packer_mod.DEFAULT_MAX_SIZE if max_size is None else max_size)
+        o.compress = 1 if compression == "LZ4" else 0
+        keybuf = knownbuf = None
+        if key is not None:
+            key = bytes(key)
+            if len(key) != 32:
+                raise ValueError("the repository key is 32 bytes (AES-256)")
+            keybuf = ctypes.create_string_buffer(key, 32)
+            o.key = ctypes.cast(keybuf, ctypes.c_void_p)
+        o.packers, o.readers, o.batch_bytes, o.timestamp = int(packers), int(readers), int(batch_bytes), int(timestamp)
+        if known:
+            ks = sorted(bytes(k) for k in known)
+            knownbuf = ctypes.create_string_buffer(b"".join(ks), 32 * len(ks))
+            o.known, o.nknown = ctypes.cast(knownbuf, ctypes.c_void_p), len(ks)
+        self._h = ctypes.c_void_p()
+        _lib.check(_lib.lib().cdc_backup_new(int(dev), ctypes.byref(o), ctypes.byref(self._h)), "cdc_backup_new")
+
+    def run(self, paths, keep_packfiles=True):
+        """Back up the files: (objects, packfiles, stats), as backup_files."""
+        import ctypes
+        from . import _lib
+        if not self._h:
+            raise ValueError("session closed")
+        n = len(paths)
+        arr = (ctypes.c_char_p * max(n, 1))(*[str(p).encode() for p in paths])
+        objects = [None] * n
+        packs = []
+        errors = []
+
+        def on_file(_ctx, fp):
+            try:
+                f = fp.contents
+                m = int(f.nchunks)
+                cuts = np.ctypeslib.as_array(ctypes.cast(f.cuts, ctypes.POINTER(ctypes.c_uint8)), (16 * m,)).view(
+                    np.dtype(_lib.CUT_DTYPE_FIELDS))
+                dg = np.ctypeslib.as_array(f.digests, (32 * m,))
+                hist = np.ctypeslib.as_array(f.hists, (256 * m,)).reshape(m, 256)
+                lens = cuts["length"].astype(np.int64)
+                ent = np.ctypeslib.as_array(f.entropy, (m,)).tolist()  # the device's entropy() per chunk
+                dist = hist / np.maximum(lens, 1)[:, None].astype(np.float64)
+                dg = dg.tobytes()
+                chunks = [hashing.Chunk(dg[32 * k:32 * k + 32], int(lens[k]), ent[k], dist[k]) for k in range(m)]
+                objects[int(f.index)] = Object(Checksum=bytes(f.checksum), Chunks=chunks,
+                                               Entropy=float(f.object_entropy))
+            except Exception as e:  # noqa: BLE001 - re-raised after the call
+                errors.append(e)
+
+        def on_pack(_ctx, data, length):
+            packs.append(ctypes.string_at(data, length) if keep_packfiles else None)
+            return 0
+
+        fcb, pcb = _lib.BACKUP_FILE_FN(on_file), _lib.BACKUP_PACK_FN(on_pack)
+        st = _lib.cdc_backup_stats()
+        _lib.check(_lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st)), "cdc_backup_files")
+        if errors:
+            raise errors[0]
+        stats = {name: getattr(st, name) for name, _ in _lib.cdc_backup_stats._fields_}
+        return objects, [p for p in packs if p is not None], stats
+
+    def close(self):
+        from . import _lib
+        if self._h:
+            _lib.lib().cdc_backup_free(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
+def backup_files(paths, repo: Repository = None, key=None, compression="LZ4", known=None, max_size=None,
+                 packers=8, readers=8, batch_bytes=256 << 20, timestamp=0, dev=0, keep_packfiles=True):
+    """One backup of a list of files through the native pipeline (a
+    BackupSession for this call only).  known: iterable of 32-byte digests
+    already in the repository (not stored again).  Returns (objects,
+    packfiles, stats): one Object per path in order (entropy and
+    Distribution computed here from the device histograms, as chunkify_batch
+    does), the serialised packfiles in the order the packers flushed them,
+    and the per-stage stats of cdc_backup_stats."""
+    with BackupSession(repo, key, compression, known, max_size, packers, readers, batch_bytes, timestamp,
+                       dev) as s:
+        return s.run(paths, keep_packfiles)
+
+
+__all__ = ["Object", "route", "chunkify_batch", "backup_batch", "BackupSession", "backup_files"]

@@ -99,3 +99,25 @@ def test_compute_entry_points_fail_loudly_without_init():
     st = L.cdc_chunk(b, 1, ctypes.byref(o), None, 0, counts, None)
     assert st in (_lib.CDC_E_NOT_INIT, _lib.CDC_E_NO_DEVICE)
     assert L.cdc_init(0, None, 0, 0, 0) == _lib.CDC_E_NO_DEVICE
+
+
+def test_host_sha256_matches_hashlib():
+    """The library's host SHA-256 (the packfile index checksum and the backup
+    pipeline's object checksums): the SHA-extension path and the portable
+    path agree with hashlib at every padding boundary and on long inputs."""
+    import ctypes
+    import hashlib
+
+    import numpy as np
+    from plakar_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, size=(1 << 20) + 333, dtype=np.uint8)
+    out = (ctypes.c_uint8 * 32)()
+    sizes = list(range(0, 200)) + [447, 448, 511, 512, 513, 4095, 4096, 65537, (1 << 20) + 333]
+    for force in (0, 1):
+        for n in sizes:
+            assert L.cdc_sha256(data.ctypes.data, n, force, out) == 0
+            assert bytes(out) == hashlib.sha256(data[:n].tobytes()).digest(), (n, force)
+    assert L.cdc_sha256(None, 1, 0, out) == _lib.CDC_E_INVALID
+    assert L.cdc_sha256_accelerated() in (0, 1)

@@ -1,0 +1,121 @@
+"""The native end-to-end backup pipeline (cdc_backup_run, snapshot.backup_files):
+files -> reads + object SHA-256 -> cut points -> chunk SHA-256 + histograms ->
+BlobExists -> Encode -> concurrent packers -> packfiles (SURVEY.md §8f rank 3;
+snapshot/backup.go:571-687, snapshot/blobs.go:9-24, snapshot/snapshot.go:51-92).
+
+Checked against the already-validated batch path (snapshot.chunkify_batch:
+cut points vs the oracle, digests vs hashlib) and by opening every packfile
+with the packfile.go restatement (tests/packfile_ref.py) and every blob with
+DecryptStream + the LZ4 reader (tests/crypto_ref.py)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import crypto_ref as ref  # noqa: E402
+import packfile_ref as pf  # noqa: E402
+from datagen import low_entropy, random_bytes  # noqa: E402
+from plakar_amd import _lib, snapshot  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+KEY = bytes(range(32, 64))
+
+
+@pytest.fixture(scope="module")
+def corpus(tmp_path_factory):
+    d = tmp_path_factory.mktemp("backup")
+    files = [b"", random_bytes(1, 1).tobytes(), random_bytes(1000, 2).tobytes(),
+             random_bytes(65535, 3).tobytes(), random_bytes(65536, 4).tobytes(), random_bytes(70_000, 5).tobytes(),
+             random_bytes(3 << 20, 6).tobytes(), low_entropy(6 << 20, 7).tobytes(), random_bytes(13 << 20, 8).tobytes()]
+    files.append(files[6])        # a duplicate file: its chunks are not stored again
+    files.append(b"")             # a second empty file: the empty chunk is stored once
+    files.append(files[8][:5 << 20] + random_bytes(1 << 20, 9).tobytes())  # shares a prefix
+    paths = []
+    for i, b in enumerate(files):
+        p = d / f"f{i:02d}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    return paths, files
+
+
+def _blobs_of(packs, key, compressed):
+    out = {}
+    for pk in packs:
+        p = pf.parse(pk)
+        for t, c, o, n in p.index:
+            assert t == 1  # TYPE_CHUNK
+            assert c not in out, "a chunk was stored twice"
+            raw = bytes(p.blobs[o:o + n])
+            out[c] = ref.decode(raw, key=key, compressed=compressed) if (key or compressed) else raw
+    return out
+
+
+@pytest.mark.parametrize("key,compression", [(KEY, "LZ4"), (None, None), (None, "LZ4")])
+def test_backup_files_matches_chunkify_and_packs_every_chunk_once(corpus, key, compression):
+    paths, files = corpus
+    objs, packs, st = snapshot.backup_files(paths, key=key, compression=compression, max_size=2 << 20,
+                                            packers=3, readers=4, batch_bytes=8 << 20, timestamp=11)
+    ref_objs = snapshot.chunkify_batch(files)
+    assert len(objs) == len(files)
+    for i, (o, r) in enumerate(zip(objs, ref_objs)):
+        assert o.Checksum == r.Checksum == hashlib.sha256(files[i]).digest(), f"file {i}"
+        assert [c.Length for c in o.Chunks] == [c.Length for c in r.Chunks], f"file {i}"
+        assert [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks], f"file {i}"
+        assert [c.Entropy for c in o.Chunks] == [c.Entropy for c in r.Chunks], f"file {i}"
+        for a, b in zip(o.Chunks, r.Chunks):
+            assert np.array_equal(a.Distribution, b.Distribution)
+        assert o.Entropy == r.Entropy
+    blobs = _blobs_of(packs, key, compression == "LZ4")
+    want = {}
+    for f, o in zip(files, objs):
+        off = 0
+        for c in o.Chunks:
+            want[c.Checksum] = f[off:off + c.Length]
+            off += c.Length
+    assert set(blobs) == set(want)
+    for c, plain in blobs.items():
+        assert plain == want[c] and hashlib.sha256(plain).digest() == c
+    assert st["files"] == len(files) and st["new_blobs"] == len(want) and st["batches"] >= 3
+    assert st["packfiles"] == len(packs) and st["bytes"] == sum(len(f) for f in files)
+    for pk in packs:  # flushed at Size() > MaxSize: no packfile holds much more than one blob past it
+        assert pf.parse(pk).timestamp == 11
+
+
+def test_backup_files_known_digests_are_skipped(corpus):
+    """BlobExists: digests the repository already holds are not stored."""
+    paths, files = corpus
+    objs, _, _ = snapshot.backup_files(paths, key=KEY)
+    every = {c.Checksum for o in objs for c in o.Chunks}
+    objs2, packs2, st2 = snapshot.backup_files(paths, key=KEY, known=every)
+    assert packs2 == [] and st2["new_blobs"] == 0
+    assert [o.Checksum for o in objs2] == [o.Checksum for o in objs]
+    some = set(list(sorted(every))[: len(every) // 2])
+    _, packs3, st3 = snapshot.backup_files(paths, key=KEY, known=some)
+    assert set(_blobs_of(packs3, KEY, True)) == every - some and st3["new_blobs"] == len(every - some)
+
+
+def test_backup_files_unreadable_path_fails_cleanly(tmp_path):
+    p = tmp_path / "ok"
+    p.write_bytes(b"x" * 100)
+    with pytest.raises(_lib.CdcError) as e:
+        snapshot.backup_files([str(p), str(tmp_path / "missing")])
+    assert e.value.status == _lib.CDC_E_IO
+
+
+def test_backup_session_reused_across_runs(corpus, tmp_path):
+    """One context, several backups: each run is a fresh backup (its own
+    dedup set), buffers grow when a later run needs more."""
+    paths, files = corpus
+    big = tmp_path / "big"
+    big.write_bytes(random_bytes(40 << 20, 123).tobytes())
+    with snapshot.BackupSession(key=KEY, batch_bytes=8 << 20, packers=2) as s:
+        o1, p1, s1 = s.run(paths[:6])
+        o2, p2, s2 = s.run(paths + [str(big)])
+        o3, p3, s3 = s.run(paths[:6])
+    assert [o.Checksum for o in o1] == [o.Checksum for o in o3]
+    assert s1["new_blobs"] == s3["new_blobs"] > 0
+    assert o2[-1].Checksum == hashlib.sha256(big.read_bytes()).digest()
+    assert set(_blobs_of(p3, KEY, True)) == {c.Checksum for o in o3 for c in o.Chunks}
