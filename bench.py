@@ -298,7 +298,7 @@ def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
     chunked = [[torch.cuda.Event() for _ in range(window)] for _ in range(2)]
     hashed = [[], []]
     wbufs = [t for _ in range(window) for t in bufs]
-    per = 32  # buffers per digest launch group (cdc_chunk_digests_device_batch_async splits there)
+    per = len(wbufs)  # one launch group per window (descriptors in device memory past 32 buffers)
 
     def one_round(r):
         w = r % 2
@@ -471,6 +471,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the multi-threaded CPU oracle leg (16 = the GPU box's CPU share; 1 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backup-readers", type=int, default=16, help="c4b: reader threads (reads + object SHA-256)")
+    ap.add_argument("--backup-packers", type=int, default=8, help="c4b: packer threads")
     ap.add_argument("--streams", type=int, default=2,
                     help="device workloads: consecutive steps alternate over this many streams, each with its "
                          "own workspace, so one batch's resolution kernels overlap the next batch's scan")
@@ -505,6 +507,12 @@ def main():
         sys.exit(2)
     if os.environ.get("BENCH_CPU_SELFTEST") == "1":
         return cpu_selftest(args, world, rank)
+    if WORKLOADS[args.workload].get("backup"):
+        # the backup pipeline's streams (H2D + cuts, digests x 2, Encode + its
+        # aux) run independently only with one hardware queue each; HIP's
+        # default of 4 queues per process shares them.  Set
+        # before the HIP runtime starts.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
     import torch
     import torch.distributed as dist
@@ -573,7 +581,8 @@ def main():
 
             if wl.get("backup"):
                 from plakar_amd import snapshot
-                session = snapshot.BackupSession(key=os.urandom(32), compression="LZ4", packers=8, readers=16,
+                session = snapshot.BackupSession(key=os.urandom(32), compression="LZ4", packers=args.backup_packers,
+                                                 readers=args.backup_readers,
                                                  dev=local)
 
                 def step():  # one whole backup of the share per step (an empty repository each time)
@@ -736,9 +745,11 @@ def main():
             bs = backup_stats[0]
             line["backup_stages"] = dict(
                 {k: (round(v, 4) if isinstance(v, float) else v) for k, v in bs.items()},
-                note="per step (the last one): seconds per stage; read_s / pack_s / objhash_s are thread times "
-                     "summed over batches or threads, device_s the calling thread's device stages; the stages "
-                     "overlap (reads of batch k+1 and packing of batch k run during batch k's device work)")
+                readers=args.backup_readers, packers=args.backup_packers,
+                GPU_MAX_HW_QUEUES=os.environ.get("GPU_MAX_HW_QUEUES"),
+                note="per step (the last one): seconds per stage; read_s / objhash_s / pack_s are thread times "
+                     "summed over threads, device_s / read_wait_s the calling thread's (read_wait_s: the device "
+                     "waiting for a batch's reads), callback_s the callback thread's; the stages overlap")
         print(json.dumps(line), flush=True)
     if host_mode and wl.get("files"):
         import shutil

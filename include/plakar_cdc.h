@@ -245,6 +245,7 @@ typedef struct cdc_backup_stats {
     double h2d_s, chunk_s, digest_s, d2h_s, encode_s;  /* device stages (events; Encode: host wall) */
     double device_s;          /* the calling thread's time in the device stages (callbacks excluded) */
     double callback_s;        /* in on_file (the callback thread) */
+    double read_wait_s;       /* the calling thread waiting for a batch's reads (device idle) */
     double pack_s;            /* packer threads' busy time, summed */
     double wall_s;
 } cdc_backup_stats;
@@ -347,7 +348,9 @@ int cdc_chunk_digests_device_async(int device, const void *d_data, uint64_t len,
                                    uint32_t *d_hist, void *stream);
 /* Batched form: every chunk of nbufs buffers hashes in one launch group (the
  * time of a launch is that of its longest chunk, so batch).  d_results and
- * d_hist may be NULL; d_hist entries are all NULL or all set. */
+ * d_hist may be NULL; d_hist entries are all NULL or all set (a buffer with
+ * cut_cap 0 may pass NULL either way).  Past 32 buffers the launch group
+ * reads its descriptors from device memory (one launch, one tail). */
 int cdc_chunk_digests_device_batch_async(int device, const void *const *d_data, const uint64_t *lens, int nbufs,
                                          const cdc_cut *const *d_cuts, const uint64_t *cut_caps,
                                          const cdc_result *const *d_results, uint8_t *const *d_digests,

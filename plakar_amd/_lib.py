@@ -68,7 +68,7 @@ class cdc_backup_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("files", "bytes", "chunks", "new_blobs", "new_bytes", "encoded_bytes",
                                                "packfiles", "packed_bytes", "batches")] + \
                [(n, ctypes.c_double) for n in ("read_s", "objhash_s", "h2d_s", "chunk_s", "digest_s", "d2h_s",
-                                               "encode_s", "device_s", "callback_s", "pack_s", "wall_s")]
+                                               "encode_s", "device_s", "callback_s", "read_wait_s", "pack_s", "wall_s")]
 
 
 BACKUP_FILE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(cdc_backup_file))

@@ -1005,14 +1005,24 @@ int cdc_chunk_digests_device_batch_async(int device, const void *const *d_data, 
                                          uint32_t *const *d_hist, void *stream)
 {
     if (nbufs < 0 || (nbufs > 0 && (!d_data || !lens || !d_cuts || !cut_caps || !d_digests))) return CDC_E_INVALID;
+    bool want_hist = false;  // histograms for all buffers or none (a buffer without chunks may pass NULL)
+    for (int i = 0; i < nbufs && d_hist; ++i) want_hist |= cut_caps[i] && d_hist[i];
     for (int i = 0; i < nbufs; ++i) {
         if ((lens[i] && !d_data[i]) || (cut_caps[i] && (!d_cuts[i] || !d_digests[i]))) return CDC_E_INVALID;
-        if (d_hist && (d_hist[i] == nullptr) != (d_hist[0] == nullptr)) return CDC_E_INVALID;
+        if (want_hist && cut_caps[i] && !d_hist[i]) return CDC_E_INVALID;
     }
+    if (!want_hist) d_hist = nullptr;
     DeviceCtx *ctx = nullptr;
     int st = check_ready(device, &ctx);
     if (st != CDC_OK) return st;
     if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    if (nbufs > kMaxBufsPerLaunch) {  // one launch group, descriptors in device memory
+        std::vector<DigestBuf> bufs(static_cast<size_t>(nbufs));
+        for (int i = 0; i < nbufs; ++i)
+            bufs[size_t(i)] = DigestBuf{static_cast<const uint8_t *>(d_data[i]), lens[i], d_cuts[i], cut_caps[i],
+                                        d_results ? d_results[i] : nullptr, d_digests[i], d_hist ? d_hist[i] : nullptr};
+        return launch_digests_many(bufs.data(), uint32_t(nbufs), stream);
+    }
     for (int i0 = 0; i0 < nbufs; i0 += kMaxBufsPerLaunch) {
         DigestBatch DB;
         std::memset(&DB, 0, sizeof(DB));

@@ -113,6 +113,7 @@ struct Slot {
     uint64_t enc_cap = 0, henc_cap = 0;
     // A: H2D start / end, cut points end; D: digests start / end, lists back
     hipEvent_t ev[6] = {};
+    hipEvent_t ev_enc = nullptr;  // E: the encoded blobs back
     // per run: lifecycle (guarded by Run::mu) and the enqueued batch's lists
     int batch = -1, next = 0;  // the batch in the slot; the one that takes it next
     bool read_done = false, hash_done = false, device_done = false;
@@ -130,7 +131,7 @@ struct Slot {
 // device and batch k - 1 is packed; with two, reads and packing serialise,
 // with three a large file's hash stalls the readers.
 constexpr int kSlots = 4;
-constexpr int kA = 0, kD = 1, kE = 2;  // cdc_backup::stream
+constexpr int kA = 0, kD = 1, kE = 3;  // cdc_backup::stream; digests alternate over kD, kD + 1
 
 #define HIPOK(x)                                         \
     do {                                                 \
@@ -162,8 +163,10 @@ int grow_host(T *&p, uint64_t need, uint64_t have)
 int grow_slot(Slot &s, uint64_t arena, uint64_t ws, uint64_t ncuts, uint64_t nfiles)
 {
     int st;
-    if (!s.ev[0])
+    if (!s.ev[0]) {
         for (auto &e : s.ev) HIPOK(hipEventCreate(&e));
+        HIPOK(hipEventCreateWithFlags(&s.ev_enc, hipEventDisableTiming));
+    }
     if (arena > s.arena_cap || !s.h_arena) {
         if ((st = grow_host(s.h_arena, arena, 0)) != CDC_OK) return st;
         uint64_t c = s.arena_cap;
@@ -214,6 +217,7 @@ void free_slot(Slot &s)
         if (p) (void)hipHostFree(p);
     for (auto &e : s.ev)
         if (e) (void)hipEventDestroy(e);
+    if (s.ev_enc) (void)hipEventDestroy(s.ev_enc);
     s = Slot();
 }
 
@@ -226,9 +230,13 @@ struct cdc_backup {
     std::vector<uint8_t> known;  // sorted digests, copied (o.known points here)
     Slot slot[kSlots];
     std::vector<cdc_packer *> packers;  // kept across runs (their buffers stay reserved and mapped)
-    // A: H2D + cut points (ahead); D: digests, entropy, lists; E: Encode and
-    // the encoded blobs back (beside the next batch's digests on D)
-    hipStream_t stream[3] = {nullptr, nullptr, nullptr};
+    // A: H2D + cut points (ahead); D0 / D1: digests, entropy, lists of even /
+    // odd batches (one batch's longest-chunk tail overlaps the next batch's
+    // digests); E: Encode and the encoded blobs back.  Four streams plus
+    // Encode's own: independent only with GPU_MAX_HW_QUEUES >= 8 (HIP's
+    // default of 4 maps several streams onto one hardware queue, which
+    // serialises them).
+    hipStream_t stream[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -258,6 +266,7 @@ struct Run {
     std::atomic<int> status{CDC_OK};
     bool stop_packers = false;
     size_t devices_done = 0;  // batches through finish_device (callbacks may start)
+    size_t cuts = 0, digs = 0;  // batches whose stage A / stage B is enqueued (the calling thread's)
     std::deque<Blob> queue;
     std::mutex sink_mu;
     std::unordered_set<Digest, DigestHash> seen;
@@ -525,7 +534,7 @@ int enqueue_digests(Run &R, size_t k)
     Slot &s = R.B->slot[k % kSlots];
     const Batch &b = R.batches[k];
     const uint32_t nf = b.f1 - b.f0;
-    hipStream_t sd = R.B->stream[kD];
+    hipStream_t sd = R.B->stream[kD + int(k & 1)];
     const auto w0 = Clock::now();
     HIPOK(hipStreamWaitEvent(sd, s.ev[2], 0));
     for (uint32_t j = 0; j < nf; ++j) {
@@ -552,6 +561,8 @@ int enqueue_digests(Run &R, size_t k)
     return CDC_OK;
 }
 
+int wait_pumping(Run &R, hipEvent_t ev, size_t k);
+
 // Batch k once its lists are back: dedup (BlobExists: the run's own chunks and
 // the caller's known digests), Encode of the new chunks on stream E, the
 // encoded blobs back, the blobs to the packers.
@@ -561,7 +572,8 @@ int finish_device(Run &R, size_t k)
     const Batch &b = R.batches[k];
     const uint32_t nf = b.f1 - b.f0;
     const auto w0 = Clock::now();
-    HIPOK(hipEventSynchronize(s.ev[5]));
+    int st = wait_pumping(R, s.ev[5], k);
+    if (st != CDC_OK) return st;
     float t[4] = {};  // H2D, cut points, digests + entropy, lists back
     HIPOK(hipEventElapsedTime(&t[0], s.ev[0], s.ev[1]));
     HIPOK(hipEventElapsedTime(&t[1], s.ev[1], s.ev[2]));
@@ -612,7 +624,6 @@ int finish_device(Run &R, size_t k)
     const bool encode = nb && (R.o.compress || R.o.key);
     std::vector<uint64_t> oo(nb + 1, 0);
     double enc_s = 0, d2h_enc_s = 0;
-    int st;
     if (encode) {
         if ((st = grow_dev(s.d_enc, s.enc_cap, enc_bound)) != CDC_OK) return st;
         std::vector<uint8_t> rnd;
@@ -631,7 +642,8 @@ int finish_device(Run &R, size_t k)
             s.henc_cap = want;
         }
         HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, R.B->stream[kE]));
-        HIPOK(hipStreamSynchronize(R.B->stream[kE]));
+        HIPOK(hipEventRecord(s.ev_enc, R.B->stream[kE]));
+        if ((st = wait_pumping(R, s.ev_enc, k)) != CDC_OK) return st;
         enc_s = secs(e0, e1);
         d2h_enc_s = secs(e1, Clock::now());
     }
@@ -724,8 +736,13 @@ void callback_main(Run &R)
 int wait_read(Run &R, size_t k)
 {
     Slot &s = R.B->slot[k % kSlots];
-    std::unique_lock<std::mutex> lk(R.mu);
-    R.cv.wait(lk, [&] { return (s.batch == int(k) && s.read_done) || R.status.load() != CDC_OK; });
+    const auto t0 = Clock::now();
+    {
+        std::unique_lock<std::mutex> lk(R.mu);
+        R.cv.wait(lk, [&] { return (s.batch == int(k) && s.read_done) || R.status.load() != CDC_OK; });
+    }
+    std::lock_guard<std::mutex> lk(R.stat_mu);
+    R.st.read_wait_s += secs(t0, Clock::now());
     return R.status.load();
 }
 
@@ -734,6 +751,32 @@ bool read_ready(Run &R, size_t k)
     Slot &s = R.B->slot[k % kSlots];
     std::lock_guard<std::mutex> lk(R.mu);
     return s.batch == int(k) && s.read_done;
+}
+
+// While batch k is on the device: stage A of every later batch whose bytes
+// are in (slots permitting) and stage B of batch k + 1 once its stage A is
+// enqueued, so the device never waits for the calling thread.
+int pump(Run &R, size_t k)
+{
+    const size_t nb = R.batches.size();
+    int st = CDC_OK;
+    while (st == CDC_OK && R.cuts < nb && R.cuts < k + kSlots && read_ready(R, R.cuts))
+        if ((st = enqueue_cuts(R, R.cuts)) == CDC_OK) ++R.cuts;
+    if (st == CDC_OK && R.digs == k + 1 && R.cuts > k + 1 && (st = enqueue_digests(R, k + 1)) == CDC_OK) ++R.digs;
+    return st;
+}
+
+// Wait for an event of batch k's, pumping the pipeline meanwhile.
+int wait_pumping(Run &R, hipEvent_t ev, size_t k)
+{
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return CDC_OK;
+        if (q != hipErrorNotReady) return CDC_E_DEVICE;
+        const int st = pump(R, k);
+        if (st != CDC_OK) return st;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
 }
 
 }  // namespace
@@ -819,32 +862,22 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
                 cdc_packer *pk = B->packers[size_t(p)];
                 packers.emplace_back([&R, pk] { packer_main(R, pk); });
             }
-            // Per batch k: stage A (H2D, cut points) of every later batch
-            // whose bytes are in (slots permitting), stage B (digests) of
-            // batch k + 1 when its stage A is enqueued, then batch k is
-            // deduplicated, Encoded and handed to the packers and the
-            // callback thread.  Nothing here waits for a read unless the
-            // device would otherwise idle.
+            // Per batch k: batch k is deduplicated, Encoded and handed to the
+            // packers and the callback thread; while this thread waits on
+            // the device it pumps (stage A of every later batch whose reads
+            // have landed, stage B of batch k + 1).  It waits for a read only
+            // when the device would otherwise idle.
             const size_t nb = R.batches.size();
-            size_t cuts = 0, digs = 0;  // batches whose stage A / stage B is enqueued
             for (size_t k = 0; k < nb && st == CDC_OK; ++k) {
-                if (digs == k) {
-                    if (cuts == k) {
+                if (R.digs == k) {
+                    if (R.cuts == k) {
                         if ((st = wait_read(R, k)) != CDC_OK || (st = enqueue_cuts(R, k)) != CDC_OK) break;
-                        ++cuts;
+                        ++R.cuts;
                     }
                     if ((st = enqueue_digests(R, k)) != CDC_OK) break;
-                    ++digs;
+                    ++R.digs;
                 }
-                while (cuts < nb && cuts < k + kSlots && read_ready(R, cuts)) {
-                    if ((st = enqueue_cuts(R, cuts)) != CDC_OK) break;
-                    ++cuts;
-                }
-                if (st != CDC_OK) break;
-                if (digs == k + 1 && cuts > k + 1) {
-                    if ((st = enqueue_digests(R, k + 1)) != CDC_OK) break;
-                    ++digs;
-                }
+                if ((st = pump(R, k)) != CDC_OK) break;
                 if ((st = finish_device(R, k)) != CDC_OK) break;
                 {
                     std::lock_guard<std::mutex> lk(R.mu);

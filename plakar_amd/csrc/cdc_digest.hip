@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
+#include <mutex>
 
 #include "cdc_internal.h"
 
@@ -137,6 +139,36 @@ constexpr uint32_t kDigestWaves = 2 * kDigestGroups;
 constexpr uint32_t kMetaLive = 1u << 9, kMetaLast = 1u << 10;  // bits 0-8: rb + 128
 constexpr uint32_t kSortCap = 1024;  // chunks a workgroup sorts longest first (8 KiB of LDS)
 
+// The workgroup's buffer: from the kernel arguments (<= 32 buffers), or from
+// device memory (launch_digests_many).
+template <bool kInd>
+__device__ __forceinline__ const DigestBuf &digest_buf(const DigestBatch &DB)
+{
+    return kInd ? DB.ind[blockIdx.y] : DB.b[blockIdx.y];
+}
+
+// Chunks of every buffer of the launch (the same value in every workgroup).
+// Descriptors in device memory: the workgroup's threads sum them in parallel.
+template <bool kInd>
+__device__ __forceinline__ uint64_t launch_chunks(const DigestBatch &DB)
+{
+    uint64_t total = 0;
+    if constexpr (!kInd) {
+        for (uint32_t j = 0; j < DB.nbufs; ++j) total += chunk_count(DB.b[j]);
+    } else {
+        __shared__ uint64_t s_part[kDigestWaves];  // this instantiation only
+        for (uint32_t j = threadIdx.x; j < DB.nbufs; j += blockDim.x) total += chunk_count(DB.ind[j]);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) total += __shfl_xor(total, o);
+        if ((threadIdx.x & 63u) == 0) s_part[threadIdx.x >> 6] = total;
+        __syncthreads();
+        total = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64u; ++w) total += s_part[w];
+    }
+    return total;
+}
+
+template <bool kInd>
 __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const DigestBatch DB)
 {
     constexpr uint32_t kLanes = 64u * kDigestGroups;
@@ -149,15 +181,14 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
     const uint32_t grp = wave % kDigestGroups;
     const uint32_t role = wave / kDigestGroups;  // 0 producer, 1 rounds
     uint4 *ring = s_ring[grp];                   // [kShaRing][16][64]
-    const DigestBuf &B = DB.b[blockIdx.y];
+    const DigestBuf &B = digest_buf<kInd>(DB);
     const uint32_t lane = threadIdx.x & 63u;
     // Chunks per workgroup: kLanes while the launch fits the resident lanes,
     // else kLanes * k, k = ceil(chunks / resident lanes) (every wave of every
     // workgroup derives the same k).  The workgroup's lanes take its chunks
     // in order from an LDS queue, a lane its next one block before its
     // current one's last.
-    uint64_t total = 0;
-    for (uint32_t j = 0; j < DB.nbufs; ++j) total += chunk_count(DB.b[j]);
+    const uint64_t total = launch_chunks<kInd>(DB);
     const uint64_t R = DB.resident_lanes ? DB.resident_lanes : 1u;
     const uint64_t k = total > R ? (total + R - 1) / R : 1u;
     const uint64_t n_cuts = chunk_count(B);
@@ -387,12 +418,13 @@ __global__ __launch_bounds__(kDigestWaves * 64) void k_chunk_digest(const Digest
 // of bins per lane, into the chunk's row.
 constexpr uint32_t kHistWaves = 4, kHistCopies = 8;
 
+template <bool kInd>
 __global__ __launch_bounds__(kHistWaves * 64) void k_chunk_hist(const DigestBatch DB)
 {
     __shared__ uint32_t s_h[kHistWaves][256 * kHistCopies];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const DigestBuf &B = DB.b[blockIdx.y];
+    const DigestBuf &B = digest_buf<kInd>(DB);
     if (!B.hist) return;
     uint32_t *h = s_h[wave];
     const uint32_t cpy = lane & (kHistCopies - 1u);
@@ -569,9 +601,55 @@ int launch_arena_cuts(const uint64_t *d_meta, uint32_t nfiles, const cdc_result 
 
 uint64_t g_digest_lanes = 0;  // cdc_debug_set_digest_lanes (0: from the device's CU count)
 
+namespace {
+
+uint32_t device_cus()
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+        n = 256;
+    return uint32_t(n);
+}
+
+template <bool kInd>
+int launch_digest_kernels(DigestBatch D, uint64_t cap, bool hist, hipStream_t st)
+{
+    static const uint32_t cus = device_cus();
+    // two SHA-256 workgroups per CU (~66 KiB of LDS each)
+    D.resident_lanes = g_digest_lanes ? g_digest_lanes : uint64_t(cus) * 2u * 64u * kDigestGroups;
+    const uint32_t lanes_per_wg = 64u * kDigestGroups;
+    hipLaunchKernelGGL(k_chunk_digest<kInd>, dim3(uint32_t((cap + lanes_per_wg - 1) / lanes_per_wg), D.nbufs),
+                       dim3(kDigestWaves * 64), 0, st, D);
+    if (hist) {  // a wave per chunk; up to 8 workgroups per CU
+        const uint64_t wgs = std::min<uint64_t>((cap + kHistWaves - 1) / kHistWaves, uint64_t(cus) * 8u);
+        hipLaunchKernelGGL(k_chunk_hist<kInd>, dim3(uint32_t(wgs), D.nbufs), dim3(kHistWaves * 64), 0, st, D);
+    }
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+}
+
+// Per-device ring of descriptor slots: pinned staging + device copy; a slot is
+// reused once the launch group that read it has finished (its event).
+constexpr uint32_t kDescRing = 16, kDescMax = 8192;
+struct DescRing {
+    std::mutex mu;
+    DigestBuf *h = nullptr, *d = nullptr;
+    hipEvent_t ev[kDescRing] = {};
+    bool used[kDescRing] = {};
+    uint32_t next = 0;
+    bool failed = false;
+};
+
+DescRing &desc_ring(int device)
+{
+    static DescRing rings[64];
+    return rings[device & 63];
+}
+
+}  // namespace
+
 int launch_digests(const DigestBatch &DB, void *stream)
 {
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     uint64_t cap = 0;
     bool hist = false;
     for (uint32_t i = 0; i < DB.nbufs; ++i) {
@@ -580,24 +658,54 @@ int launch_digests(const DigestBatch &DB, void *stream)
     }
     if (cap == 0 || DB.nbufs == 0) return CDC_OK;
     if (cap > 0xFFFFFFFFull) return CDC_E_INVALID;  // chunk indices relative to a workgroup's first are u32
-    static const uint32_t cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return uint32_t(n);
-    }();
-    // two SHA-256 workgroups per CU (~66 KiB of LDS each)
     DigestBatch D = DB;
-    D.resident_lanes = g_digest_lanes ? g_digest_lanes : uint64_t(cus) * 2u * 64u * kDigestGroups;
-    const uint32_t lanes_per_wg = 64u * kDigestGroups;
-    hipLaunchKernelGGL(k_chunk_digest, dim3(uint32_t((cap + lanes_per_wg - 1) / lanes_per_wg), DB.nbufs),
-                       dim3(kDigestWaves * 64), 0, st, D);
-    if (hist) {  // a wave per chunk; up to 8 workgroups per CU
-        const uint64_t wgs = std::min<uint64_t>((cap + kHistWaves - 1) / kHistWaves, uint64_t(cus) * 8u);
-        hipLaunchKernelGGL(k_chunk_hist, dim3(uint32_t(wgs), DB.nbufs), dim3(kHistWaves * 64), 0, st, D);
+    D.ind = nullptr;
+    return launch_digest_kernels<false>(D, cap, hist, reinterpret_cast<hipStream_t>(stream));
+}
+
+int launch_digests_many(const DigestBuf *bufs, uint32_t nbufs, void *stream)
+{
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return CDC_E_DEVICE;
+    DescRing &R = desc_ring(dev);
+    for (uint32_t i0 = 0; i0 < nbufs; i0 += kDescMax) {
+        const uint32_t n = std::min(kDescMax, nbufs - i0);
+        uint64_t cap = 0;
+        bool hist = false;
+        for (uint32_t i = 0; i < n; ++i) {
+            cap = std::max(cap, bufs[i0 + i].cap);
+            hist |= bufs[i0 + i].hist != nullptr;
+        }
+        if (cap == 0) continue;
+        if (cap > 0xFFFFFFFFull) return CDC_E_INVALID;
+        std::lock_guard<std::mutex> lk(R.mu);
+        if (!R.h) {
+            if (R.failed) return CDC_E_DEVICE;
+            const size_t bytes = size_t(kDescRing) * kDescMax * sizeof(DigestBuf);
+            bool ok = hipHostMalloc(reinterpret_cast<void **>(&R.h), bytes, hipHostMallocDefault) == hipSuccess &&
+                      hipMalloc(reinterpret_cast<void **>(&R.d), bytes) == hipSuccess;
+            for (auto &e : R.ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (!ok) {
+                R.failed = true;  // leave it unusable rather than half made
+                return CDC_E_DEVICE;
+            }
+        }
+        const uint32_t slot = R.next++ % kDescRing;
+        if (R.used[slot] && hipEventSynchronize(R.ev[slot]) != hipSuccess) return CDC_E_DEVICE;
+        DigestBuf *h = R.h + size_t(slot) * kDescMax, *d = R.d + size_t(slot) * kDescMax;
+        std::memcpy(h, bufs + i0, n * sizeof(DigestBuf));
+        if (hipMemcpyAsync(d, h, n * sizeof(DigestBuf), hipMemcpyHostToDevice, st) != hipSuccess) return CDC_E_DEVICE;
+        DigestBatch D;
+        std::memset(&D, 0, sizeof(D));
+        D.nbufs = n;
+        D.ind = d;
+        int s2 = launch_digest_kernels<true>(D, cap, hist, st);
+        if (s2 != CDC_OK) return s2;
+        if (hipEventRecord(R.ev[slot], st) != hipSuccess) return CDC_E_DEVICE;
+        R.used[slot] = true;
     }
-    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+    return CDC_OK;
 }
 
 }  // namespace cdc

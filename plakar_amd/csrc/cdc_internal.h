@@ -120,9 +120,14 @@ struct DigestBuf {
 struct DigestBatch {
     uint32_t nbufs;
     uint64_t resident_lanes;  // lanes the device keeps resident at once (set by launch_digests)
+    const DigestBuf *ind;     // launch_digests_many: the nbufs descriptors in device memory (b unused)
     DigestBuf b[kMaxBufsPerLaunch];
 };
 int launch_digests(const DigestBatch &DB, void *stream);
+// More than kMaxBufsPerLaunch buffers in ONE launch group: the descriptors go
+// to device memory through a per-device pinned ring (a launch lasts as long as
+// its longest chunk, so several groups of 32 would each pay that tail).
+int launch_digests_many(const DigestBuf *bufs, uint32_t nbufs, void *stream);
 int launch_entropy(const uint32_t *d_hist, uint64_t rows, double *d_out, void *stream);
 int launch_arena_cuts(const uint64_t *d_meta, uint32_t nfiles, const cdc_result *d_res, const cdc_cut *d_cuts,
                       cdc_cut *d_out, void *stream);

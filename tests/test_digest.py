@@ -262,6 +262,47 @@ def test_gpu_digest_multi_chunk_lanes(lanes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nbufs,lanes", [(33, 0), (300, 0), (70, 64)])
+def test_gpu_digest_many_buffers_one_launch_group(nbufs, lanes):
+    """More than 32 buffers in one call: one launch group whose descriptors
+    live in device memory (launch_digests_many), empty buffers and empty cut
+    lists among them, counts bounded by result rows on every third; repeated
+    calls cycle the descriptor ring past its 16 slots."""
+    torch = _gpu()
+    from plakar_amd import _lib, hashing
+    _lib.ensure_init()
+    L = _lib.lib()
+    refs = []
+    for k in range(nbufs):
+        n = 0 if k % 17 == 5 else 1000 + (k * 7919) % 90000
+        b = random_bytes(n, 900 + k)
+        cuts, o = [], 0
+        while o < n:
+            m = min(n - o, 100 + (o * 2654435761 + k) % 9000)
+            cuts.append((o, m))
+            o += m
+        if k % 11 == 3:
+            cuts.append((0, 0))
+        refs.append((b, cuts))
+    try:
+        if lanes:
+            assert L.cdc_debug_set_digest_lanes(lanes) == 0
+        bufs = [torch.from_numpy(np.ascontiguousarray(b)).cuda() if b.size else torch.zeros(1, dtype=torch.uint8,
+                                                                                            device="cuda")
+                for b, _ in refs]
+        cls = [torch.tensor(np.asarray(c, np.int64).reshape(-1, 2), device="cuda") for _, c in refs]
+        keeps = [len(c) - 1 if (i % 3 == 0 and c) else len(c) for i, (_, c) in enumerate(refs)]
+        res = [torch.tensor([kp, 0, 0, 0], dtype=torch.int64, device="cuda") for kp in keeps]
+        for _ in range(3 if nbufs < 100 else 1):
+            outs = hashing.chunk_digests_batch(bufs, cls, res)
+        torch.cuda.synchronize()
+    finally:
+        L.cdc_debug_set_digest_lanes(0)
+    for (b, c), kp, (d, h) in zip(refs, keeps, outs):
+        _check(b, c[:kp], d[:kp].cpu().numpy(), h[:kp].cpu().numpy())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lanes", [1, 128, 700])
 def test_gpu_digest_queue_order(lanes):
     """Workgroups with more chunks than lanes: up to 1,024 of them handed out
