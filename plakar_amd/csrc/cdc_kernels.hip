@@ -588,6 +588,12 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     using C1 = std::integral_constant<uint32_t, 1>;
 
     uint4 A[4] = {}, Bv[4] = {};
+#ifdef CDC_DIAG_WAITS
+    // build-time diagnostic only: shader cycles this wave spends in the
+    // per-stage DMA waits, and its whole task, to g_ts[kTsRes + 2 task]
+    uint64_t wsum = 0;
+    const uint64_t tk0 = __builtin_amdgcn_s_memtime();
+#endif
     // Stage 0 is not rolled: it lies 128 B (half 0) or 192 B (half 1) before
     // the run, and stage 1 alone gives fp >= 64 >= W - 1 warm-up bytes.  Its
     // loads and DMA issues are kept.
@@ -619,7 +625,13 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
 #pragma unroll
         for (uint32_t gi = 0; gi < kGroups; ++gi) {
             if (gi + 1 == kGroups && t + 1 < TT) {
+#ifdef CDC_DIAG_WAITS
+                const uint64_t w0 = __builtin_amdgcn_s_memtime();
                 wait_vmcnt<0>();  // DMA t + 1 landed
+                wsum += __builtin_amdgcn_s_memtime() - w0;
+#else
+                wait_vmcnt<0>();  // DMA t + 1 landed
+#endif
                 if (half != Q) load_row(nxt_d, cur_d);
                 asm volatile("" ::: "memory");
             }
@@ -656,8 +668,16 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+#ifndef CDC_DIAG_NO_RECHECK
             if (acc == 0) [[unlikely]]
                 recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
+#else
+            rec += acc == 0 ? 1u : 0u;  // build-time diagnostic only: no recheck
+            (void)f0;
+#if CDC_DIAG_NO_RECHECK == 2
+            if (acc == 0) [[unlikely]] asm volatile("s_nop 0" ::: "memory");  // the branch alone
+#endif
+#endif
             if constexpr (kFused) {
                 if (accL == 0) [[unlikely]]
                     record_l_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, lws, vlm, recL);
@@ -675,6 +695,12 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
         if (lane == 0) W.validL[task] = 1u;
     }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
+#ifdef CDC_DIAG_WAITS
+    if (lane == 0 && 2 * task + 1 < 8 * 16384) {
+        g_ts[kTsRes + 2 * task] = wsum;
+        g_ts[kTsRes + 2 * task + 1] = __builtin_amdgcn_s_memtime() - tk0;
+    }
+#endif
 }
 
 __global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
