@@ -103,6 +103,14 @@ def main():
     slow = np.argsort(r[:, 2] - r[:, 0])[-4:]
     print("  slowest speculative chains (segment: us, exact calls, listed): " +
           ", ".join(f"{i}: {(r[i, 2] - r[i, 0]) / 100.0:.1f}, {r[i, 6]}, {r[i, 5]}" for i in slow))
+    slow8 = np.argsort(r[:, 2])[-8:]
+    print("  latest spec exits (segment: start, build us, walk us, exact, listed, exit at): " +
+          "; ".join(f"{i}: {us(r[i, 0]):.1f}, {(r[i, 1] - r[i, 0]) / 100.0:.1f}, {(r[i, 2] - r[i, 1]) / 100.0:.1f}, "
+                    f"{r[i, 6]}, {r[i, 5]}, {us(r[i, 2]):.1f}" for i in slow8))
+    ex = r[:, 6] > 0
+    if ex.any():
+        print(f"  walk us with exact calls {pct((r[ex, 2] - r[ex, 1]) / 100.0)} ({int(ex.sum())} segs); "
+              f"without {pct((r[~ex, 2] - r[~ex, 1]) / 100.0)}")
     lbs = np.argsort(r[:, 3])[-4:]
     print("  latest look-backs (segment: done at us): " + ", ".join(f"{i}: {us(r[i, 3]):.1f}" for i in lbs))
     print(f"  listed nodes {pct(r[:, 5])}   exact next_node() calls {pct(r[:, 6])}   junction nodes {pct(r[:, 7])}")
