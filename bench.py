@@ -701,6 +701,17 @@ def main():
                            path="cdc_chunk: pageable host -> H2D (runtime-staged) -> kernels -> D2H cut lists",
                            sample=f"{len(host)} x {host[0].size / GIB:.3g} GiB, {args.e2e_reps} reps",
                            same_cuts_as_device_path=same)
+                # the same bytes from pinned host memory (north_star's "pinned hipMemcpyAsync" form)
+                pinned = [torch.empty(t.numel(), dtype=torch.uint8, pin_memory=True) for t in bufs[:1]]
+                for p, t in zip(pinned, bufs[:1]):
+                    p.copy_(t)
+                hostp = [p.numpy() for p in pinned]
+                rate_p, sec_p, cuts_p = e2e_host_rate(chunkers, opts, hostp, args.e2e_reps)
+                same_p = all(a.shape == d.shape and bool((a == d).all()) for a, d in zip(cuts_p, dev_cuts))
+                e2e["pinned"] = dict(value=round(rate_p, 2), unit="GiB/s", ms_per_call=round(sec_p * 1e3, 2),
+                                     path="cdc_chunk: pinned host -> H2D (direct DMA) -> kernels -> D2H cut lists",
+                                     same_cuts_as_device_path=same_p)
+                del hostp, pinned
             sample = host
             sample_cuts = cuts[:1]
         if not args.no_cpu_baseline:
