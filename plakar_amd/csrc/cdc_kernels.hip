@@ -573,7 +573,13 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
         constexpr uint32_t Q = decltype(PC)::value;  // u & 1: the half this DMA feeds
         const uint64_t adv = uint64_t(kStage) * (u - Q) + (Q ? half_step : 0ull);
         if (om0 + adv <= uint64_t(lim)) {
+#ifdef CDC_DIAG_L2
+            // build-time diagnostic only: every DMA reads a 512-KiB window of
+            // the buffer (L2-resident), wrong bytes, the scan's compute alone
+            dma_stage(lo_ok + ((base + adv - lo_ok) & 0x7FFF0ull), ring, off0);
+#else
             dma_stage(base + adv, ring, off0);
+#endif
         } else {
             uint32_t eff[4];
 #pragma unroll

@@ -52,6 +52,33 @@ __device__ __forceinline__ void dma4(uint64_t base_in, uint32_t dst_in, const ui
                  : "memory", "scc");
 }
 
+// 4x4 transpose of 16-B pieces within each lane quad: before, lane 4q+i
+// register k holds piece i of run 16k+q; after, lane 4q+i register k holds
+// piece k of run 16i+q.  Two butterfly stages (xor 1, xor 2 lanes), each a
+// DPP quad_perm read of the partner's register and a per-lane select.
+__device__ __forceinline__ uint32_t qperm1(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }  // [1,0,3,2]
+__device__ __forceinline__ uint32_t qperm2(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }  // [2,3,0,1]
+__device__ __forceinline__ void quad_transpose(uint4 (&r)[4], uint32_t lane)
+{
+    const bool b0 = lane & 1u, b1 = lane & 2u;
+    auto xch = [&](uint4 &lo, uint4 &hi, bool b, auto perm) {
+        // b = 0: lo keeps, hi <- partner's lo;  b = 1: lo <- partner's hi, hi keeps
+        uint32_t *pl = reinterpret_cast<uint32_t *>(&lo), *ph = reinterpret_cast<uint32_t *>(&hi);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t send = b ? pl[d] : ph[d];
+            const uint32_t recv = perm(send);
+            const uint32_t nl = b ? recv : pl[d], nh = b ? ph[d] : recv;
+            pl[d] = nl;
+            ph[d] = nh;
+        }
+    };
+    xch(r[0], r[1], b0, qperm1);
+    xch(r[2], r[3], b0, qperm1);
+    xch(r[0], r[2], b1, qperm2);
+    xch(r[1], r[3], b1, qperm2);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(W * 64) void kern(const uint8_t *buf, uint32_t *out, uint64_t *cyc, int stages,
                                                uint32_t vhi)
@@ -69,29 +96,43 @@ __global__ __launch_bounds__(W * 64) void kern(const uint8_t *buf, uint32_t *out
     for (int j = 0; j < 4; ++j) off[j] = (8 * j + lane / 8) * SL + 16 * (lane % 8);
     const char *rowp = s + 256 * 32 * 8 + wave * 4096 + (lane & 31) * 128;
     const uint8_t *myrun = buf + uint64_t(gw) * 64 * SL + uint64_t(lane) * SL;
+    // MODE 6-8: quad loads (lane 4q+i: piece i of run 16k+q); 7/8: every wave reads the same 360-KiB region
+    const uint8_t *wreg = (MODE == 7 || MODE == 8) ? buf : buf + uint64_t(gw) * 64 * SL;
+    auto qload = [&](uint4 (&r)[4], int st) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            r[k] = *reinterpret_cast<const uint4 *>(wreg + uint64_t(16 * k + lane / 4) * SL + 64 * (st % 88) + 16 * (lane % 4));
+    };
     uint4 d = make_uint4(threadIdx.x * 0x01010101u, threadIdx.x * 0x3u + 7, blockIdx.x, 0x12345678u);
     uint4 cur[4], nxt[4];
-    if (MODE >= 4)
+    if (MODE == 4 || MODE == 5)
         for (int j = 0; j < 4; ++j) cur[j] = *reinterpret_cast<const uint4 *>(myrun + 16 * j);
+    if (MODE == 6 || MODE == 7) {
+        qload(cur, 0);
+        quad_transpose(cur, lane);
+    }
     uint64_t gv[2][16];
     for (int k = 0; k < 16; ++k) gv[0][k] = *reinterpret_cast<const uint64_t *>(t + gear_addr(laneoff, word_of(d, k >> 2), k));
     uint64_t fp = 0;
     uint32_t hits = 0, sink = 0;
-    if (MODE == 1 || MODE == 2) dma4(wbase, ring, off);
+    const uint64_t dbase = MODE == 8 ? reinterpret_cast<uint64_t>(buf) : wbase;
+    if (MODE == 1 || MODE == 2 || MODE == 8) dma4(dbase, ring, off);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     for (int st = 0; st < stages; ++st) {
-        if (MODE >= 4) {
+        if (MODE == 4 || MODE == 5) {
             const int sn = st + 1 < stages ? st + 1 : st;
 #pragma unroll
             for (int j = 0; j < 4; ++j) nxt[j] = *reinterpret_cast<const uint4 *>(myrun + 64 * (sn % 88) + 16 * j);
         }
+        if (MODE == 6 || MODE == 7) qload(nxt, st + 1 < stages ? st + 1 : st);
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) {
             uint64_t (&cg)[16] = gv[gi & 1];
             uint64_t (&ng)[16] = gv[(gi & 1) ^ 1];
-            if (gi == 3 && (MODE == 1 || MODE == 2)) {
+            if (gi == 3 && (MODE == 6 || MODE == 7)) quad_transpose(nxt, lane);
+            if (gi == 3 && (MODE == 1 || MODE == 2 || MODE == 8)) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (MODE == 2 && (lane >> 5) == (uint32_t(st) & 1)) {
+                if ((MODE == 2 || MODE == 8) && (lane >> 5) == (uint32_t(st) & 1)) {
                     uint4 r[8];
 #pragma unroll
                     for (int g = 0; g < 8; ++g) r[g] = *reinterpret_cast<const uint4 *>(rowp + 16 * (g ^ ((lane >> 1) & 7)));
@@ -99,7 +140,7 @@ __global__ __launch_bounds__(W * 64) void kern(const uint8_t *buf, uint32_t *out
                     for (int g = 0; g < 8; ++g) sink ^= r[g].x ^ r[g].w;
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                dma4(wbase + uint64_t(((st + 1) / 2) % 44) * 128 + uint64_t((st + 1) & 1) * 32ull * SL, ring, off);
+                dma4(dbase + uint64_t(((st + 1) / 2) % 44) * 128 + uint64_t((st + 1) & 1) * 32ull * SL, ring, off);
             }
             if (gi == 3 && MODE == 3 && (lane >> 5) == (uint32_t(st) & 1)) {
                 uint4 r[8];
@@ -109,7 +150,7 @@ __global__ __launch_bounds__(W * 64) void kern(const uint8_t *buf, uint32_t *out
                 for (int g = 0; g < 8; ++g) sink ^= r[g].x ^ r[g].w;
             }
             uint4 nx;
-            if (MODE == 5) nx = gi < 3 ? cur[gi + 1] : nxt[0];
+            if (MODE == 5 || MODE == 6 || MODE == 7) nx = gi < 3 ? cur[gi + 1] : nxt[0];
             else nx = make_uint4(d.x + uint32_t(st * 4 + gi) * 0x9E3779B9u, d.y ^ uint32_t(st), d.z + uint32_t(gi), d.w ^ (uint32_t(st) << 7));
             uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
@@ -126,7 +167,7 @@ __global__ __launch_bounds__(W * 64) void kern(const uint8_t *buf, uint32_t *out
             }
             if (acc == 0) ++hits;
         }
-        if (MODE >= 4) {
+        if (MODE >= 4 && MODE <= 7) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (MODE == 4) sink ^= cur[j].x ^ cur[j].z;
@@ -182,6 +223,10 @@ int main()
     run<3>("3 + row reads only", buf, out, cyc);
     run<4>("4 + direct loads (unused)", buf, out, cyc);
     run<5>("5 direct loads feed the loop", buf, out, cyc);
+    run<6>("6 quad loads + DPP transpose", buf, out, cyc);
+    run<7>("7 = 6, L2-resident region", buf, out, cyc);
+    run<8>("8 = 2 (LDS-DMA), L2-resident region", buf, out, cyc);
+    run<3>("3 row reads only (again)", buf, out, cyc);
     run<0>("0 bare loop (again)", buf, out, cyc);
     return 0;
 }
