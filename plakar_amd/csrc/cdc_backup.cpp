@@ -25,7 +25,7 @@
 //   packer threads   Packer.AddBlob into their own packfile (cdc_packer_*),
 //                    flush at Size() > MaxSize to the packfile callback
 //                    (PutPackfile)
-// Four slots (arena + device buffers) rotate, so later batches are read while
+// Six slots (arena + device buffers) rotate, so later batches are read while
 // batch k is on the device and earlier ones are packed; the per-file
 // callbacks run on their own thread while the device takes the next batches.
 #include <hip/hip_runtime.h>
@@ -126,11 +126,16 @@ struct Slot {
     std::vector<uint64_t> file_new0;   // per file: its first entry in is_new
 };
 
-// Four slots: batches k + 1 .. k + 3 are read (and object-hashed: a 128-MiB
-// file is one ~64-ms SHA-256 chain on a host core) while batch k is on the
-// device and batch k - 1 is packed; with two, reads and packing serialise,
-// with three a large file's hash stalls the readers.
-constexpr int kSlots = 4;
+// Six slots: batches k + 1 .. k + 5 are read (and object-hashed: a 128-MiB
+// file is one ~64-ms SHA-256 chain on a host core, and a slot is released
+// only once every object hash of its batch is done) while batch k is on the
+// device and earlier ones are packed; with two, reads and packing serialise;
+// with four the device idled for tens of ms behind a large file's hash (c4b
+// 10.1-11.3 GiB/s against 13.3-14.2 with six; eight no better).
+#ifndef CDC_BACKUP_SLOTS
+#define CDC_BACKUP_SLOTS 6
+#endif
+constexpr int kSlots = CDC_BACKUP_SLOTS;
 constexpr int kA = 0, kD = 1, kE = 3;  // cdc_backup::stream; digests alternate over kD, kD + 1
 
 #define HIPOK(x)                                         \
