@@ -512,7 +512,7 @@ def main():
         # aux) run independently only with one hardware queue each; HIP's
         # default of 4 queues per process shares them.  Set
         # before the HIP runtime starts.
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"  # the box exports HIP's default of 4
 
     import torch
     import torch.distributed as dist
