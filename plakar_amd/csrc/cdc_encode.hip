@@ -730,6 +730,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_enc_plan(const Batch B)
     __shared__ uint32_t s_p[kPlanThreads / 64];
     __shared__ uint64_t s_carry_o;
     __shared__ uint32_t s_carry_p;
+    if (threadIdx.x == 0) B.status[1] = 0;  // k_gcm's piece counter
     if (threadIdx.x == 0) {
         s_carry_o = 0;
         s_carry_p = 0;
@@ -1216,11 +1217,19 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     }
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, laneoff = lane << 2;
     const char *te = reinterpret_cast<const char *>(L.te);
-    const uint32_t pc = blockIdx.x * kGcmWaves + wv;
+    __syncthreads();
+    // Persistent: one workgroup per CU; each wave takes pieces from a counter
+    // (B.status[1], zeroed by k_enc_plan) until none is left, so the last
+    // round of pieces does not leave most CUs idle.
     const uint32_t total = B.piece_base[B.nblobs];
-    const bool active = pc < total && !B.status[0];
-    uint32_t b = 0;
-    if (active) {
+    if (B.status[0]) return;
+    for (;;) {
+    uint32_t pc = 0;
+    if (lane == 0) pc = atomicAdd(reinterpret_cast<uint32_t *>(&B.status[1]), 1u);
+    pc = uint32_t(__builtin_amdgcn_readfirstlane(int(pc)));
+    if (pc >= total) break;
+    uint32_t b;
+    {
         uint32_t lo = 0, hi = B.nblobs;  // last blob with piece_base <= pc
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -1229,12 +1238,14 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         }
         b = lo;
         const BlobKey &K = B.keys[b];
+        // this wave's tables (the previous piece's reads of them are done: the
+        // wave barrier at the end of its loop body)
         for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk[i] = K.rk[i];
         if (lane < 16) L.w[wv].th[lane] = K.th[lane];
         for (uint32_t i = lane; i < 256; i += 64) L.w[wv].t64[i] = K.t64[i];
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
-    if (!active) return;
     const BlobKey &K = B.keys[b];
     const uint32_t k = pc - B.piece_base[b];
     const uint64_t F = B.frame_len[b];
@@ -1336,6 +1347,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             tag[8 + q] = uint8_t(lo >> (56 - 8 * q));
         }
     }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1368,6 +1382,19 @@ static int ensure_tables()
 }
 
 static uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+
+// k_gcm's persistent grid: one workgroup per CU (its LDS holds one).
+static uint64_t gcm_wgs()
+{
+    static const uint64_t n = [] {
+        int c = 0, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        return uint64_t(c);
+    }();
+    return n;
+}
 
 // Workspace kept per device between calls (grow-only); a call holds its
 // device's lock while it runs (the entry point is synchronous).
@@ -1447,7 +1474,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
                  o_sout = take(ng * 4);
     const size_t o_bsz = take(nk * 4), o_bfo = take(nk * 8), o_xxh = take(nb * 4), o_flen = take(nb * 8);
     const size_t o_oo = take((nb + 1) * 8), o_pb = take((nb + 1) * 4), o_keys = take(encrypt ? nb * sizeof(BlobKey) : 0);
-    const size_t o_status = take(8), o_frames = take(encrypt ? slot : 0), o_xx = take(compress ? nb * 4 : 0);
+    const size_t o_status = take(16), o_frames = take(encrypt ? slot : 0), o_xx = take(compress ? nb * 4 : 0);
     if (device < 0 || device >= 64) return CDC_E_INVALID;
     WsCache &C = g_ws[device];
     std::lock_guard<std::mutex> lk(C.mu);
@@ -1542,7 +1569,8 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
             hipLaunchKernelGGL(k_copy, dim3(n), dim3(256), 0, s, Bt);
         }
         if (encrypt && pieces_max)
-            hipLaunchKernelGGL(k_gcm, dim3(uint32_t((pieces_max + kGcmWaves - 1) / kGcmWaves)), dim3(kGcmWaves * 64), 0, s, Bt);
+            hipLaunchKernelGGL(k_gcm, dim3(uint32_t(std::min<uint64_t>((pieces_max + kGcmWaves - 1) / kGcmWaves, gcm_wgs()))),
+                               dim3(kGcmWaves * 64), 0, s, Bt);
         ok = hipGetLastError() == hipSuccess;
     }
     uint64_t status = 0;
