@@ -132,8 +132,9 @@ int cdc_chunk(const cdc_buf *bufs, int nbufs, const cdc_opts *opts, cdc_cut *out
  * plakar chunks each file in its own goroutine (snapshot/backup.go:216-225,
  * each running the Next() loop of backup.go:647-665).  A collector takes such
  * per-file calls from any number of threads and submits them to the devices
- * as batches: a batch closes at batch_bytes (0: 256 MiB), at 64 files, or
- * max_wait_us after its first file arrived; each batch is one cdc_chunk.
+ * as batches: a batch closes at batch_bytes (0: 256 MiB), at 32 files, or
+ * max_wait_us after its first file arrived; each device runs its batches
+ * through a two-slot pipeline (batch k + 1 staged while batch k is chunked).
  * cdc_collector_chunk blocks until the caller's own cut list is back and has
  * cdc_chunk's contract for one buffer (CDC_E_NOSPACE with *count set when cap
  * is too small).  cdc_collector_free drains pending calls, then stops. */
