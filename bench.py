@@ -391,6 +391,76 @@ def cpu_threads_leg(orc, gear, kw, bufs_host, threads, seconds):
                        f"in {el:.1f} s, {threads} threads")
 
 
+def parity_check(bufs_host, cuts, opts, budget_bytes=1 << 30):
+    """This rank's cut lists against the CPU oracle on a bounded sample (the
+    first buffers, up to ~1 GiB): True iff every sampled list is bit-identical.
+    Runs after the timed region on every rank; the line reports the AND over
+    ranks."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_ref import Oracle
+    from plakar_amd import _lib
+    orc, gear = Oracle(), _lib.default_gear()
+    kw = dict(min_size=opts.MinSize, normal_size=opts.NormalSize, max_size=opts.MaxSize)
+    ok, done = True, 0
+    for a, c in zip(bufs_host, cuts):
+        if done >= budget_bytes:
+            break
+        ref = orc.chunk(a, gear, **kw)
+        got = np.asarray(c.cpu().numpy() if hasattr(c, "cpu") else c).astype(np.uint64)
+        ok &= bool(got.shape == ref.shape and (got == ref).all())
+        done += a.size
+    return ok, done
+
+
+def reduce_and(dist, world, flag, dev):
+    """AND over ranks of a host bool (None counts as False)."""
+    if world == 1:
+        return bool(flag)
+    import torch
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def backup_cpu_baseline(paths, opts, threads, key, compress=True):
+    """c4b's CPU baseline: the same backup of the same files on host cores
+    (oracle/backup_cpu.c: pread, object SHA-256, the C oracle's chunkify,
+    per-chunk SHA-256 + histogram + entropy, BlobExists, LZ4 frame +
+    AES-256-GCM stream, packfile serialisation; OpenSSL + liblz4), `threads`
+    worker threads taking files in turn (the reference's goroutine per file).
+    Warm page cache, as the GPU leg."""
+    import numpy as np
+    from plakar_amd import _lib
+
+    class Params(ctypes.Structure):
+        _fields_ = [("gear", ctypes.c_void_p), ("mask_s", ctypes.c_uint64), ("mask_l", ctypes.c_uint64),
+                    ("min_size", ctypes.c_uint64), ("normal_size", ctypes.c_uint64), ("max_size", ctypes.c_uint64),
+                    ("cut_adj", ctypes.c_uint32)]
+
+    class Stats(ctypes.Structure):
+        _fields_ = [(n, ctypes.c_uint64) for n in ("files", "bytes", "chunks", "new_blobs", "encoded_bytes",
+                                                   "packfiles", "packed_bytes", "failed_files")] + \
+                   [("wall_s", ctypes.c_double)]
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libbackup_cpu.so"))
+    lib.backup_cpu_run.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Params),
+                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(Stats)]
+    gear = np.ascontiguousarray(_lib.default_gear(), dtype=np.uint64)
+    P = Params(gear.ctypes.data, 0x0003590703530000, 0x0000d90003530000, opts.MinSize, opts.NormalSize,
+               opts.MaxSize, 0)
+    arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+    kb = ctypes.create_string_buffer(bytes(key), 32) if key else None
+    st = Stats()
+    assert lib.backup_cpu_run(arr, len(paths), threads, ctypes.byref(P), kb, 1 if compress else 0, 20 << 20,
+                              ctypes.byref(st)) == 0
+    return dict(value=round(st.bytes / st.wall_s / GIB, 3), unit="GiB/s", cores=threads, kind="port",
+                chunks=st.chunks, new_blobs=st.new_blobs,
+                sample=f"the same {st.files} files ({st.bytes / GIB:.2f} GiB), one whole backup in {st.wall_s:.2f} s, "
+                       f"{threads} threads (oracle/backup_cpu.c: pread, object SHA-256, the C oracle's chunkify, "
+                       f"chunk SHA-256 + histogram + entropy, dedup, LZ4 frame + AES-256-GCM stream, packfiles; "
+                       f"OpenSSL libcrypto + liblz4), warm page cache, nproc={os.cpu_count()}")
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -450,9 +520,29 @@ def cpu_selftest(args, world, rank):
         dist.barrier()
     elapsed = reduce_max(dist, world, el, None)
     per = gather_per_rank(dist, world, el, None)
+    # the post-timed legs of a real run, on host bytes: every rank checks its
+    # own (CPU-oracle) cut lists of a small sample, the line carries the AND;
+    # rank 0 times the CPU baseline at any N
+    import numpy as np
+    from plakar_amd import chunkers
+    opts = chunkers.ChunkerOpts(MinSize=64 * 1024, NormalSize=1 << 20, MaxSize=4 << 20)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_ref import Oracle
+    from plakar_amd import _lib
+    host = [np.random.PCG64(1 + rank).random_raw(1 << 20).view(np.uint8)]
+    cuts = [Oracle().chunk(host[0], _lib.default_gear(), min_size=opts.MinSize, normal_size=opts.NormalSize,
+                           max_size=opts.MaxSize)]
+    if os.environ.get("BENCH_SELFTEST_BAD_RANK") == str(rank):
+        cuts = [cuts[0][:-1]]  # a wrong list on one rank must turn the AND false
+    ok, _ = parity_check(host, cuts, opts)
+    parity = reduce_and(dist, world, ok, None)
+    baseline = None
+    if rank == 0:
+        baseline, _ = cpu_baseline(host, cuts, opts, 0.2, threads=1)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "selftest": True,
-                          "elapsed_max_s": elapsed, "per_rank_elapsed_s": per}), flush=True)
+                          "elapsed_max_s": elapsed, "per_rank_elapsed_s": per,
+                          "parity_vs_oracle": parity, "cpu_baseline": baseline}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -471,6 +561,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the multi-threaded CPU oracle leg (16 = the GPU box's CPU share; 1 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the per-rank oracle check after the timed region")
     ap.add_argument("--backup-readers", type=int, default=16, help="c4b: reader threads (reads + object SHA-256)")
     ap.add_argument("--backup-packers", type=int, default=8, help="c4b: packer threads")
     ap.add_argument("--streams", type=int, default=2,
@@ -512,7 +603,12 @@ def main():
         # aux) run independently only with one hardware queue each; HIP's
         # default of 4 queues per process shares them.  Set
         # before the HIP runtime starts.
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"  # the box exports HIP's default of 4
+        # The GPU box exports HIP's default of 4; the line records the value
+        # found and the one applied (BENCH_KEEP_HW_QUEUES=1 measures with the
+        # value found, as a host that does not set it would run).
+        os.environ["BENCH_GPU_MAX_HW_QUEUES_GIVEN"] = os.environ.get("GPU_MAX_HW_QUEUES", "")
+        if os.environ.get("BENCH_KEEP_HW_QUEUES") != "1":
+            os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
     import torch
     import torch.distributed as dist
@@ -581,7 +677,8 @@ def main():
 
             if wl.get("backup"):
                 from plakar_amd import snapshot
-                session = snapshot.BackupSession(key=os.urandom(32), compression="LZ4", packers=args.backup_packers,
+                session_key = os.urandom(32)
+                session = snapshot.BackupSession(key=session_key, compression="LZ4", packers=args.backup_packers,
                                                  readers=args.backup_readers,
                                                  dev=local)
 
@@ -673,16 +770,28 @@ def main():
 
     digest = None
     if not host_mode and args.digest_reps > 0:
-        digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0 and world == 1)
+        digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0)
         digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_window, 8)
 
     encode_res = None
     if not host_mode and args.encode_reps > 0:
-        encode_res = encode_leg(torch, batch, bufs, args.encode_reps, rank == 0 and world == 1)
+        encode_res = encode_leg(torch, batch, bufs, args.encode_reps, rank == 0)
 
-    baseline, parity, e2e = None, None, None
-    if rank == 0 and world == 1:
-        import numpy as np
+    # Every rank checks its own cut lists (a bounded sample, ~1 GiB) against
+    # the CPU oracle; the line carries the AND over ranks.  Rank 0 also times
+    # the CPU baseline, at any N (not part of `value`).
+    import numpy as np
+    if args.no_parity:
+        parity = None
+    elif host_mode:
+        parity, _ = parity_check(host_bufs, host_cuts, opts)
+    else:
+        parity, _ = parity_check([t.cpu().numpy() for t in bufs[:max(1, (1 << 30) // max(1, bufs[0].numel()))]],
+                                 cuts, opts)
+    if parity is not None:
+        parity = reduce_and(dist, world, parity, dev)
+    baseline, e2e = None, None
+    if rank == 0:
         if host_mode:
             sample, tot = [], 0
             for a in host_bufs:  # bounded sample: the first ~1 GiB of the corpus
@@ -714,8 +823,13 @@ def main():
                 del hostp, pinned
             sample = host
             sample_cuts = cuts[:1]
-        if not args.no_cpu_baseline:
-            baseline, parity = cpu_baseline(sample, sample_cuts, opts, args.cpu_seconds, args.cpu_threads)
+        if not args.no_cpu_baseline and wl.get("backup"):
+            baseline = backup_cpu_baseline(paths, opts, max(1, args.cpu_threads), session_key)
+            # the chunker alone on 1 core over the same sample, as the other workloads report it
+            baseline["chunker_only_1_core"], _ = cpu_baseline(sample, sample_cuts, opts, args.cpu_seconds / 2, 1)
+        elif not args.no_cpu_baseline:
+            baseline, sample_ok = cpu_baseline(sample, sample_cuts, opts, args.cpu_seconds, args.cpu_threads)
+            baseline["sample_parity"] = sample_ok
 
     if rank == 0:
         config = {"workload": wl["desc"], "bytes_per_gpu": per_rank_bytes,
@@ -758,6 +872,7 @@ def main():
                 {k: (round(v, 4) if isinstance(v, float) else v) for k, v in bs.items()},
                 readers=args.backup_readers, packers=args.backup_packers,
                 GPU_MAX_HW_QUEUES=os.environ.get("GPU_MAX_HW_QUEUES"),
+                GPU_MAX_HW_QUEUES_given=os.environ.get("BENCH_GPU_MAX_HW_QUEUES_GIVEN") or None,
                 note="per step (the last one): seconds per stage; read_s / objhash_s / pack_s are thread times "
                      "summed over threads, device_s / read_wait_s the calling thread's (read_wait_s: the device "
                      "waiting for a batch's reads), callback_s the callback thread's; the stages overlap")

@@ -212,8 +212,18 @@ void cdc_packer_free(cdc_packer *p);
  * drives the next batches through the device), with pointers valid during the
  * call only; chunk entropies come from the device (cdc_chunk_entropy_device_async).
  * An empty file is one empty chunk (backup.go:631-635); a file shorter than
- * MinSize is one chunk.  Returns the first failure (CDC_E_IO for a file that
- * cannot be read, a negative status from on_pack). */
+ * MinSize is one chunk.  A file larger than the batch size is processed in
+ * pieces of about batch_bytes, in order, each chunked from the previous
+ * piece's carried chunk start (the cut points are those of the whole file),
+ * so the pinned and device buffers stay bounded by batch_bytes + Max per slot
+ * whatever the file sizes; on_file is then called once per piece (piece /
+ * pieces; cut offsets are file-relative; checksum and object_entropy are set
+ * in the last piece's call).  A file that cannot be read (missing, not a
+ * regular file, shorter than when it was listed) is reported through on_file
+ * with status CDC_E_IO and no chunks, and the backup goes on with the others
+ * (backupCtx.recordError, snapshot/backup.go:264-267); stats.failed_files
+ * counts them.  Returns CDC_OK, or the first failure of the run itself (a
+ * device error, a negative status from on_pack). */
 typedef struct cdc_backup_opts {
     cdc_opts chunking;
     uint32_t packfile_max;
@@ -238,6 +248,7 @@ typedef struct cdc_backup_file {
     const uint8_t *is_new;    /* 1: stored by this run (PutBlob), 0: deduplicated */
     const double *entropy;    /* per chunk (Chunk.Entropy: entropy() with Go's math.Log2) */
     double object_entropy;    /* Object.Entropy: sum of entropy * length in chunk order / size */
+    uint32_t piece, pieces;   /* this call's piece of the file (pieces == 1: the whole file) */
 } cdc_backup_file;
 typedef struct cdc_backup_stats {
     uint64_t files, bytes, chunks, new_blobs, new_bytes, encoded_bytes, packfiles, packed_bytes, batches;
@@ -249,6 +260,15 @@ typedef struct cdc_backup_stats {
     double read_wait_s;       /* the calling thread waiting for a batch's reads (device idle) */
     double pack_s;            /* packer threads' busy time, summed */
     double wall_s;
+    uint64_t failed_files;    /* files reported with status CDC_E_IO */
+    uint64_t pieces;          /* units through the pipeline (files + extra pieces of large files) */
+    uint64_t slot_arena_bytes;  /* pinned arena bytes per slot this run needed (<= batch_bytes + Max) */
+    /* GPU_MAX_HW_QUEUES in the process environment at cdc_backup_new (0: unset,
+     * HIP's default of 4).  The pipeline's four streams + Encode's side stream
+     * run independently only with >= 8 hardware queues; with fewer, HIP maps
+     * several streams onto one queue and the stages serialise. */
+    int32_t hw_queues;
+    int32_t streams_serialised;  /* 1 when hw_queues < 8 (or unset) */
 } cdc_backup_stats;
 typedef void (*cdc_backup_file_fn)(void *ctx, const cdc_backup_file *f);
 typedef int (*cdc_backup_pack_fn)(void *ctx, const uint8_t *packfile, uint64_t len);

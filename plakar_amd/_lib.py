@@ -61,14 +61,16 @@ class cdc_backup_file(ctypes.Structure):
                 ("size", ctypes.c_uint64), ("nchunks", ctypes.c_uint64), ("cuts", ctypes.POINTER(cdc_cut)),
                 ("digests", ctypes.POINTER(ctypes.c_uint8)), ("hists", ctypes.POINTER(ctypes.c_uint32)),
                 ("is_new", ctypes.POINTER(ctypes.c_uint8)), ("entropy", ctypes.POINTER(ctypes.c_double)),
-                ("object_entropy", ctypes.c_double)]
+                ("object_entropy", ctypes.c_double), ("piece", ctypes.c_uint32), ("pieces", ctypes.c_uint32)]
 
 
 class cdc_backup_stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("files", "bytes", "chunks", "new_blobs", "new_bytes", "encoded_bytes",
                                                "packfiles", "packed_bytes", "batches")] + \
                [(n, ctypes.c_double) for n in ("read_s", "objhash_s", "h2d_s", "chunk_s", "digest_s", "d2h_s",
-                                               "encode_s", "device_s", "callback_s", "read_wait_s", "pack_s", "wall_s")]
+                                               "encode_s", "device_s", "callback_s", "read_wait_s", "pack_s", "wall_s")] + \
+               [(n, ctypes.c_uint64) for n in ("failed_files", "pieces", "slot_arena_bytes")] + \
+               [("hw_queues", ctypes.c_int32), ("streams_serialised", ctypes.c_int32)]
 
 
 BACKUP_FILE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(cdc_backup_file))

@@ -40,6 +40,7 @@
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -70,14 +71,17 @@ struct DigestHash {
     }
 };
 
-int read_exact(const char *path, uint8_t *dst, uint64_t len)
+// Bytes [off, off + len) of the file; CDC_E_IO if it cannot be opened or ends
+// early (a file that shrank since plan() stat'ed it).
+int read_exact(const char *path, uint8_t *dst, uint64_t off, uint64_t len)
 {
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return CDC_E_IO;
     uint64_t got = 0;
     int st = CDC_OK;
     while (got < len) {
-        const ssize_t k = pread(fd, dst + got, size_t(std::min<uint64_t>(len - got, 1ull << 30)), off_t(got));
+        const ssize_t k =
+            pread(fd, dst + got, size_t(std::min<uint64_t>(len - got, 1ull << 30)), off_t(off + got));
         if (k < 0 && errno == EINTR) continue;
         if (k <= 0) {
             st = CDC_E_IO;
@@ -89,10 +93,40 @@ int read_exact(const char *path, uint8_t *dst, uint64_t len)
     return st;
 }
 
+// A unit is one file, or one piece of a file larger than the batch size
+// (batch_bytes): piece j adds the file's bytes [nb, ne) = [j P, min((j + 1) P,
+// size)) and is chunked from the previous piece's carried next start (at most
+// Max - 1 bytes before nb) to ne, non-final except the last piece, so every
+// slot's arena stays at most P + Max bytes whatever the file sizes (the
+// reference streams a file through its chunker in the same way,
+// snapshot/backup.go:647-665).  Pieces of one file run in order: piece j is
+// read once piece j - 1's cut list is back.
+struct Unit {
+    uint32_t file, piece, pieces;
+    uint64_t nb, ne;       // nominal byte range of the file (what the object hash adds)
+    uint64_t cap;          // arena bytes reserved (256-B aligned)
+    uint64_t arena_off;
+    uint64_t start = 0, len = 0;  // set by the reader: file bytes [start, start + len) in the arena
+    int err = CDC_OK;             // set by the reader: CDC_E_IO (the file could not be read)
+};
+
+// Per file, shared by its pieces (guarded by Run::mu unless noted).
+struct FileState {
+    uint64_t size = 0;
+    int err = CDC_OK;             // the first failure of any of its pieces
+    uint32_t dev_pieces = 0;      // pieces whose carried next start is published
+    uint32_t hashed_pieces = 0;   // pieces whose bytes went into the object hash
+    uint64_t next_start = 0;
+    cdc::Sha256 sha;              // multi-piece files (the reader of the current piece)
+    uint8_t obj[32] = {};         // the object checksum
+    double ent_acc = 0.0;         // Object.Entropy's running sum (callback thread)
+    bool ent_any = false;
+};
+
 struct Batch {
-    uint32_t f0, f1;      // files [f0, f1)
-    uint64_t bytes;       // arena bytes (files 256-B aligned)
-    uint64_t cuts_cap;    // sum of len / Min + 2
+    uint32_t u0, u1;      // units [u0, u1)
+    uint64_t bytes;       // arena bytes (units 256-B aligned)
+    uint64_t cuts_cap;    // sum of cap / Min + 2
 };
 
 // Buffers of one pipeline slot.  Kept by the context across runs and grown
@@ -242,6 +276,7 @@ struct cdc_backup {
     // default of 4 maps several streams onto one hardware queue, which
     // serialises them).
     hipStream_t stream[4] = {nullptr, nullptr, nullptr, nullptr};
+    int hw_queues = 0;  // GPU_MAX_HW_QUEUES at cdc_backup_new (0: unset)
 };
 
 namespace {
@@ -261,11 +296,11 @@ struct Run {
     cdc_backup_file_fn on_file;
     cdc_backup_pack_fn on_pack;
     void *ctx;
-    std::vector<uint64_t> size, arena_off;
+    std::vector<FileState> files;
+    std::vector<Unit> units;
     std::vector<Batch> batches;
-    std::vector<uint32_t> batch_of;  // per file
-    std::atomic<uint32_t> next_file{0};
-    std::vector<Digest> obj;  // per file
+    std::vector<uint32_t> batch_of;  // per unit
+    std::atomic<uint32_t> next_unit{0};
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
@@ -294,37 +329,60 @@ struct Run {
 int plan(Run &R, uint64_t &arena_cap, uint64_t &cuts_cap, uint64_t &ws_cap, uint64_t &files_cap)
 {
     const uint64_t bb = R.o.batch_bytes ? R.o.batch_bytes : (256ull << 20);
-    R.size.resize(size_t(R.n));
-    R.arena_off.resize(size_t(R.n));
-    R.obj.resize(size_t(R.n));
-    R.batch_of.resize(size_t(R.n));
-    Batch cur{0, 0, 0, 0};
+    const uint64_t P = std::max<uint64_t>(bb, 4ull * R.o.chunking.max_size);  // piece size (>> Max)
+    R.files.resize(size_t(R.n));
     for (int i = 0; i < R.n; ++i) {
+        FileState &F = R.files[size_t(i)];
         struct stat sb;
-        if (!R.paths[i] || stat(R.paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) return CDC_E_IO;
-        const uint64_t len = uint64_t(sb.st_size);
-        const uint64_t need = (len + 255) & ~255ull;
-        if (cur.f1 > cur.f0 && (cur.bytes + need > bb || cur.f1 - cur.f0 >= 4096)) {
-            R.batches.push_back(cur);
-            cur = Batch{uint32_t(i), uint32_t(i), 0, 0};
+        // a path that cannot be stat'ed or is not a regular file: that file
+        // fails (status CDC_E_IO in its record), the others go on, as
+        // backupCtx.recordError does (snapshot/backup.go:264-267)
+        if (!R.paths[i] || stat(R.paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) F.err = CDC_E_IO;
+        else F.size = uint64_t(sb.st_size);
+        const uint32_t pieces = F.size > P ? uint32_t((F.size + P - 1) / P) : 1u;
+        for (uint32_t j = 0; j < pieces; ++j) {
+            Unit u;
+            u.file = uint32_t(i);
+            u.piece = j;
+            u.pieces = pieces;
+            u.nb = pieces == 1 ? 0 : uint64_t(j) * P;
+            u.ne = pieces == 1 ? F.size : std::min<uint64_t>(F.size, uint64_t(j + 1) * P);
+            u.cap = ((u.ne - u.nb) + (j ? R.o.chunking.max_size : 0) + 255) & ~255ull;
+            R.units.push_back(u);
         }
-        R.size[size_t(i)] = len;
-        R.batch_of[size_t(i)] = uint32_t(R.batches.size());
-        R.arena_off[size_t(i)] = cur.bytes;
-        cur.bytes += need;
-        cur.cuts_cap += len / R.o.chunking.min_size + 2;
-        cur.f1 = uint32_t(i + 1);
     }
-    if (cur.f1 > cur.f0) R.batches.push_back(cur);
+    R.batch_of.resize(R.units.size());
+    Batch cur{0, 0, 0, 0};
+    for (uint32_t k = 0; k < uint32_t(R.units.size()); ++k) {
+        Unit &u = R.units[k];
+        if (cur.u1 > cur.u0 && (cur.bytes + u.cap > bb || cur.u1 - cur.u0 >= 4096)) {
+            R.batches.push_back(cur);
+            cur = Batch{k, k, 0, 0};
+        }
+        R.batch_of[k] = uint32_t(R.batches.size());
+        u.arena_off = cur.bytes;
+        cur.bytes += u.cap;
+        cur.cuts_cap += u.cap / R.o.chunking.min_size + 2;
+        cur.u1 = k + 1;
+    }
+    if (cur.u1 > cur.u0) R.batches.push_back(cur);
     arena_cap = cuts_cap = ws_cap = files_cap = 0;
+    std::vector<uint64_t> caps;
     for (const Batch &b : R.batches) {
         arena_cap = std::max(arena_cap, std::max<uint64_t>(b.bytes, 256));
         cuts_cap = std::max(cuts_cap, b.cuts_cap);
-        files_cap = std::max<uint64_t>(files_cap, b.f1 - b.f0);
-        for (uint32_t g = b.f0; g < b.f1; g += cdc::kMaxBufsPerLaunch) {
-            const uint32_t e = std::min<uint32_t>(b.f1, g + cdc::kMaxBufsPerLaunch);
+        files_cap = std::max<uint64_t>(files_cap, b.u1 - b.u0);
+        for (uint32_t g = b.u0; g < b.u1; g += cdc::kMaxBufsPerLaunch) {
+            const uint32_t e = std::min<uint32_t>(b.u1, g + cdc::kMaxBufsPerLaunch);
+            caps.clear();
+            for (uint32_t k = g; k < e; ++k) {
+                const Unit &u = R.units[k];
+                // a non-final piece is chunked alone in its batch (one launch, final = 0)
+                if (u.piece + 1 < u.pieces && b.u1 - b.u0 != 1) return CDC_E_INVALID;
+                caps.push_back(u.cap);
+            }
             uint64_t ws = 0;
-            const int s = cdc_device_batch_workspace_size(R.size.data() + g, int(e - g), &R.o.chunking, &ws);
+            const int s = cdc_device_batch_workspace_size(caps.data(), int(e - g), &R.o.chunking, &ws);
             if (s != CDC_OK) return s;
             ws_cap = std::max(ws_cap, ws);
         }
@@ -342,18 +400,24 @@ void maybe_release(Run &R, Slot &s)
     }
 }
 
-// Reader threads: file after file in batch order (a slot is claimed by the
-// first file of its batch once the batch three back released it), each file
+// Reader threads: unit after unit in batch order (a slot is claimed by the
+// first unit of its batch once the batch kSlots back released it), each unit
 // read into the slot's arena and then hashed there (the object checksum, one
 // serial chain: a large file's hash no longer holds back the batch's reads or
-// the next batch; it gates only the callbacks and the slot's release).
+// the next batch; it gates only the callbacks and the slot's release).  Piece
+// j > 0 of a large file waits for piece j - 1's carried next start (its cut
+// list back from the device) before it reads, and for piece j - 1's hash
+// before it continues the object hash.  A file that cannot be read is marked
+// failed and the run goes on.
 void reader_main(Run &R)
 {
     double read_s = 0, hash_s = 0;
-    for (uint32_t i; (i = R.next_file.fetch_add(1)) < uint32_t(R.n) && R.status.load() == CDC_OK;) {
+    for (uint32_t i; (i = R.next_unit.fetch_add(1)) < uint32_t(R.units.size()) && R.status.load() == CDC_OK;) {
         const uint32_t k = R.batch_of[i];
         const Batch &b = R.batches[k];
         Slot &s = R.B->slot[k % kSlots];
+        Unit &u = R.units[i];
+        FileState &F = R.files[u.file];
         {
             std::unique_lock<std::mutex> lk(R.mu);
             R.cv.wait(lk, [&] {
@@ -367,34 +431,55 @@ void reader_main(Run &R)
                 s.nread = s.nhashed = 0;
                 s.pending = 0;
             }
+            if (u.piece)  // the previous piece's cut list is back (or the file failed)
+                R.cv.wait(lk, [&] { return R.status.load() != CDC_OK || F.err != CDC_OK || F.dev_pieces >= u.piece; });
+            if (R.status.load() != CDC_OK) break;
+            u.err = F.err;
+            u.start = u.piece ? F.next_start : 0;
+            u.len = u.err == CDC_OK ? u.ne - u.start : 0;
         }
-        uint8_t *dst = s.h_arena + R.arena_off[i];
+        uint8_t *dst = s.h_arena + u.arena_off;
         const auto t0 = Clock::now();
-        const int st = read_exact(R.paths[i], dst, R.size[i]);
+        int st = u.err == CDC_OK ? read_exact(R.paths[u.file], dst, u.start, u.len) : CDC_OK;
         const auto t1 = Clock::now();
         read_s += secs(t0, t1);
-        if (st != CDC_OK) {
-            R.fail(st);
-            break;
-        }
         bool wake;
         {
             std::lock_guard<std::mutex> lk(R.mu);
-            wake = ++s.nread == b.f1 - b.f0;
+            if (st != CDC_OK) {
+                u.err = st;
+                u.len = 0;
+                if (F.err == CDC_OK) F.err = st;
+            }
+            wake = ++s.nread == b.u1 - b.u0;
             s.read_done = s.read_done || wake;
         }
-        if (wake) R.cv.notify_all();
-        cdc::sha256(dst, R.size[i], R.obj[i].b);
+        R.cv.notify_all();
+        if (u.err == CDC_OK && u.pieces == 1) {
+            cdc::sha256(dst, u.len, F.obj);
+        } else if (u.pieces > 1) {
+            bool go;
+            {
+                std::unique_lock<std::mutex> lk(R.mu);
+                R.cv.wait(lk, [&] { return R.status.load() != CDC_OK || F.hashed_pieces >= u.piece; });
+                go = F.err == CDC_OK && u.err == CDC_OK && R.status.load() == CDC_OK;
+            }
+            if (go) {  // the bytes this piece adds: [nb, ne) of the file
+                F.sha.update(dst + (u.nb - u.start), size_t(u.ne - u.nb));
+                if (u.piece + 1 == u.pieces) F.sha.final(F.obj);
+            }
+        }
         hash_s += secs(t1, Clock::now());
         {
             std::lock_guard<std::mutex> lk(R.mu);
-            wake = ++s.nhashed == b.f1 - b.f0;
+            if (u.pieces > 1) F.hashed_pieces = u.piece + 1;
+            wake = ++s.nhashed == b.u1 - b.u0;
             if (wake) {
                 s.hash_done = true;
                 maybe_release(R, s);
             }
         }
-        if (wake) R.cv.notify_all();
+        R.cv.notify_all();
     }
     std::lock_guard<std::mutex> lk(R.stat_mu);
     R.st.read_s += read_s;
@@ -468,15 +553,16 @@ int random_bytes(uint8_t *p, size_t n)
 // Object.Entropy (snapshot/backup.go:612-627, 668-670): totalEntropy +=
 // entropy * float64(len) over the chunks in order, then / float64(size); one
 // IEEE operation at a time.
+// The running sum continues across the pieces of a large file (chunk order is
+// file order); the caller divides by the size after the last piece.
 #pragma clang fp contract(off)
-double object_entropy(const double *e, const cdc_cut *cuts, uint64_t n, uint64_t size)
+void object_entropy_add(double &acc, bool &any, const double *e, const cdc_cut *cuts, uint64_t n)
 {
-    double acc = 0.0;
     for (uint64_t i = 0; i < n; ++i) {
         const double t = e[i] * double(cuts[i].length);
-        acc = i ? acc + t : t;
+        acc = any ? acc + t : t;
+        any = true;
     }
-    return size ? acc / double(size) : 0.0;
 }
 #pragma clang fp contract(on)
 
@@ -493,7 +579,7 @@ int enqueue_cuts(Run &R, size_t k)
     Slot &s = R.B->slot[k % kSlots];
     const Batch &b = R.batches[k];
     const cdc_opts *co = &R.o.chunking;
-    const uint32_t nf = b.f1 - b.f0;
+    const uint32_t nf = b.u1 - b.u0;
     hipStream_t st1 = R.B->stream[kA];
     const auto w0 = Clock::now();
     HIPOK(hipEventRecord(s.ev[0], st1));
@@ -507,19 +593,24 @@ int enqueue_cuts(Run &R, size_t k)
     s.cut0.assign(nf, 0);
     uint64_t c = 0;
     for (uint32_t j = 0; j < nf; ++j) {
-        const uint32_t i = b.f0 + j;
-        dp[j] = s.d_in + R.arena_off[i];
-        s.lens[j] = R.size[i];
-        caps[j] = R.size[i] / co->min_size + 2;
+        const Unit &u = R.units[b.u0 + j];
+        dp[j] = s.d_in + u.arena_off;
+        s.lens[j] = u.len;  // 0 for a file that failed (no chunk) and for an empty one (one empty chunk)
+        caps[j] = u.len / co->min_size + 2;
         s.cut0[j] = c;
         cp[j] = s.d_cuts + c;
         rp[j] = s.d_res + j;
         c += caps[j];
     }
     s.ncut = c;
+    // a piece before a file's last is chunked non-final (plan() puts it alone
+    // in its batch): its cut list stops at the last chunk whose window lies
+    // inside the piece, and the rest is carried into the next piece
+    const Unit &u0 = R.units[b.u0];
+    const int final_ = u0.piece + 1 < u0.pieces ? 0 : 1;
     for (uint32_t g = 0; g < nf; g += cdc::kMaxBufsPerLaunch) {
         const int m = int(std::min<uint32_t>(cdc::kMaxBufsPerLaunch, nf - g));
-        const int st = cdc_chunk_device_batch_async(R.B->device, dp.data() + g, s.lens.data() + g, m, 1, co,
+        const int st = cdc_chunk_device_batch_async(R.B->device, dp.data() + g, s.lens.data() + g, m, final_, co,
                                                     cp.data() + g, caps.data() + g, rp.data() + g, s.d_ws, s.ws_cap,
                                                     st1);
         if (st != CDC_OK) return st;
@@ -538,14 +629,14 @@ int enqueue_digests(Run &R, size_t k)
 {
     Slot &s = R.B->slot[k % kSlots];
     const Batch &b = R.batches[k];
-    const uint32_t nf = b.f1 - b.f0;
+    const uint32_t nf = b.u1 - b.u0;
     hipStream_t sd = R.B->stream[kD + int(k & 1)];
     const auto w0 = Clock::now();
     HIPOK(hipStreamWaitEvent(sd, s.ev[2], 0));
     for (uint32_t j = 0; j < nf; ++j) {
         s.h_meta[3 * j] = s.cut0[j];
         s.h_meta[3 * j + 1] = s.lens[j] / R.o.chunking.min_size + 2;
-        s.h_meta[3 * j + 2] = R.arena_off[b.f0 + j];
+        s.h_meta[3 * j + 2] = R.units[b.u0 + j].arena_off;
     }
     const uint64_t c = s.ncut;
     HIPOK(hipEventRecord(s.ev[3], sd));
@@ -575,10 +666,24 @@ int finish_device(Run &R, size_t k)
 {
     Slot &s = R.B->slot[k % kSlots];
     const Batch &b = R.batches[k];
-    const uint32_t nf = b.f1 - b.f0;
+    const uint32_t nf = b.u1 - b.u0;
     const auto w0 = Clock::now();
     int st = wait_pumping(R, s.ev[5], k);
     if (st != CDC_OK) return st;
+    {  // a non-final piece: publish where the next piece starts (its reader waits for it)
+        const Unit &u = R.units[b.u0];
+        if (u.piece + 1 < u.pieces) {
+            std::lock_guard<std::mutex> lk(R.mu);
+            FileState &F = R.files[u.file];
+            if (u.err == CDC_OK && s.h_res[0].status == CDC_OK) {
+                F.next_start = u.start + s.h_res[0].consumed;
+                // a piece of P >> Max bytes always emits a chunk; the carry is < Max
+                if (F.next_start <= u.start || u.ne - F.next_start >= R.o.chunking.max_size) return CDC_E_DEVICE;
+            }
+            F.dev_pieces = u.piece + 1;
+        }
+    }
+    R.cv.notify_all();
     float t[4] = {};  // H2D, cut points, digests + entropy, lists back
     HIPOK(hipEventElapsedTime(&t[0], s.ev[0], s.ev[1]));
     HIPOK(hipEventElapsedTime(&t[1], s.ev[1], s.ev[2]));
@@ -597,18 +702,27 @@ int finish_device(Run &R, size_t k)
     is_new.clear();
     file_new0.assign(nf, 0);
     uint64_t enc_bound = 0, nchunks = 0, new_bytes = 0;
+    uint64_t nfiles = 0, nbytes = 0, nfailed = 0;
     for (uint32_t j = 0; j < nf; ++j) {
         const cdc_result &r = s.h_res[j];
+        const Unit &u = R.units[b.u0 + j];
         if (s.lens[j] && r.status != CDC_OK) return int(r.status);
         file_new0[j] = is_new.size();
-        const uint64_t cn = s.lens[j] ? r.ncuts : 1;  // an empty file is one empty chunk (backup.go:631-635)
+        if (u.piece + 1 == u.pieces) {
+            ++nfiles;
+            nfailed += u.err != CDC_OK ? 1 : 0;
+        }
+        if (u.err == CDC_OK) nbytes += u.ne - u.nb;
+        // an empty file is one empty chunk (backup.go:631-635); a file that
+        // failed has none
+        const uint64_t cn = s.lens[j] ? r.ncuts : u.err == CDC_OK ? 1 : 0;
         for (uint64_t q = 0; q < cn; ++q) {
             Digest d;
             uint64_t off = 0, len = 0;
             if (s.lens[j]) {
                 const cdc_cut &cc = s.h_cuts[s.cut0[j] + q];
                 std::memcpy(d.b, s.h_dig + 32 * (s.cut0[j] + q), 32);
-                off = R.arena_off[b.f0 + j] + cc.offset;
+                off = u.arena_off + cc.offset;
                 len = cc.length;
             } else {
                 std::memcpy(d.b, kEmptySum, 32);
@@ -664,8 +778,10 @@ int finish_device(Run &R, size_t k)
     R.cv.notify_all();
     std::lock_guard<std::mutex> lk(R.stat_mu);
     R.st.batches += 1;
-    R.st.files += nf;
-    for (uint32_t j = 0; j < nf; ++j) R.st.bytes += s.lens[j];
+    R.st.files += nfiles;
+    R.st.failed_files += nfailed;
+    R.st.pieces += nf;
+    R.st.bytes += nbytes;
     R.st.chunks += nchunks;
     R.st.new_blobs += nb;
     R.st.new_bytes += new_bytes;
@@ -686,7 +802,7 @@ int finish_host(Run &R, size_t k)
 {
     Slot &s = R.B->slot[k % kSlots];
     const Batch &b = R.batches[k];
-    const uint32_t nf = b.f1 - b.f0;
+    const uint32_t nf = b.u1 - b.u0;
     {
         std::unique_lock<std::mutex> lk(R.mu);  // the batch's lists + dedup, and every object checksum
         R.cv.wait(lk, [&] { return (R.devices_done > k && s.hash_done) || R.status.load() != CDC_OK; });
@@ -698,20 +814,45 @@ int finish_host(Run &R, size_t k)
         static const uint32_t kZeroHist[256] = {};
         static const double kZeroEnt[1] = {0.0};
         for (uint32_t j = 0; j < nf; ++j) {
+            const Unit &u = R.units[b.u0 + j];
+            FileState &F = R.files[u.file];
             cdc_backup_file f;
             std::memset(&f, 0, sizeof(f));
-            f.index = int(b.f0 + j);
-            f.status = CDC_OK;
-            std::memcpy(f.checksum, R.obj[b.f0 + j].b, 32);
-            f.size = s.lens[j];
-            const bool empty = s.lens[j] == 0;
-            f.nchunks = empty ? 1 : s.h_res[j].ncuts;
-            f.cuts = empty ? &kEmptyCut : s.h_cuts + s.cut0[j];
-            f.digests = empty ? kEmptySum : s.h_dig + 32 * s.cut0[j];
-            f.hists = empty ? kZeroHist : s.h_hist + 256 * s.cut0[j];
+            f.index = int(u.file);
+            f.piece = u.piece;
+            f.pieces = u.pieces;
+            f.size = F.size;
+            const bool last = u.piece + 1 == u.pieces;
+            int err;
+            {
+                std::lock_guard<std::mutex> lk(R.mu);
+                err = u.err != CDC_OK ? u.err : (last ? F.err : CDC_OK);
+            }
+            f.status = err;
+            if (u.err != CDC_OK) {  // no chunk: the file (or this piece of it) could not be read
+                f.nchunks = 0;
+            } else if (s.lens[j] == 0) {
+                f.nchunks = 1;
+                f.cuts = &kEmptyCut;
+                f.digests = kEmptySum;
+                f.hists = kZeroHist;
+                f.entropy = kZeroEnt;
+            } else {
+                f.nchunks = s.h_res[j].ncuts;
+                cdc_cut *c = s.h_cuts + s.cut0[j];
+                if (u.start)  // file-relative offsets for a piece after the first
+                    for (uint64_t q = 0; q < f.nchunks; ++q) c[q].offset += u.start;
+                f.cuts = c;
+                f.digests = s.h_dig + 32 * s.cut0[j];
+                f.hists = s.h_hist + 256 * s.cut0[j];
+                f.entropy = s.h_ent + s.cut0[j];
+                object_entropy_add(F.ent_acc, F.ent_any, f.entropy, f.cuts, f.nchunks);
+            }
             f.is_new = s.is_new.data() + s.file_new0[j];
-            f.entropy = empty ? kZeroEnt : s.h_ent + s.cut0[j];
-            f.object_entropy = empty ? 0.0 : object_entropy(f.entropy, f.cuts, f.nchunks, f.size);
+            if (last && err == CDC_OK) {
+                std::memcpy(f.checksum, F.obj, 32);
+                f.object_entropy = F.size ? F.ent_acc / double(F.size) : 0.0;
+            }
             R.on_file(R.ctx, &f);
         }
     }
@@ -813,6 +954,7 @@ int cdc_backup_new(int device, const cdc_backup_opts *opts, cdc_backup **out)
         delete b;
         return CDC_E_NOMEM;
     }
+    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES")) b->hw_queues = std::atoi(q);
     bool ok = hipSetDevice(device) == hipSuccess;
     for (auto &sm : b->stream) ok = ok && hipStreamCreateWithFlags(&sm, hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
@@ -840,6 +982,7 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
     try {
         uint64_t arena = 0, ncuts = 0, ws = 0, nfiles = 0;
         st = plan(R, arena, ncuts, ws, nfiles);
+        R.st.slot_arena_bytes = arena;
         if (st == CDC_OK && hipSetDevice(B->device) != hipSuccess) st = CDC_E_DEVICE;
         for (int i = 0; i < kSlots && st == CDC_OK && !R.batches.empty(); ++i) {
             st = grow_slot(B->slot[i], arena, ws, ncuts, nfiles);
@@ -916,6 +1059,8 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
         for (auto &sm : B->stream) (void)hipStreamSynchronize(sm);
     }
     R.st.wall_s = secs(w0, Clock::now());
+    R.st.hw_queues = B->hw_queues;
+    R.st.streams_serialised = B->hw_queues < 8 ? 1 : 0;
     if (stats) *stats = R.st;
     delete Rp;
     return st;

@@ -606,9 +606,11 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     uint4 A[4] = {}, Bv[4] = {};
 #ifdef CDC_DIAG_WAITS
     // build-time diagnostic only: shader cycles this wave spends in the
-    // per-stage DMA waits, and its whole task, to g_ts[kTsRes + 2 task]
+    // per-stage DMA waits, its whole task and where it ran, to g_ts[kTsRes + 8 task]
     uint64_t wsum = 0;
+    uint32_t nrc = 0;  // groups whose filter fired in some lane (wave-uniform branch count)
     const uint64_t tk0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     // Stage 0 is not rolled: it lies 128 B (half 0) or 192 B (half 1) before
     // the run, and stage 1 alone gives fp >= 64 >= W - 1 warm-up bytes.  Its
@@ -685,6 +687,9 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
                 }
             }
 #ifndef CDC_DIAG_NO_RECHECK
+#ifdef CDC_DIAG_WAITS
+            nrc += __builtin_amdgcn_readfirstlane(uint32_t(__ballot(acc == 0) != 0));
+#endif
             if (acc == 0) [[unlikely]]
                 recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
 #else
@@ -716,9 +721,18 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 #ifdef CDC_DIAG_WAITS
-    if (lane == 0 && 2 * task + 1 < 8 * 16384) {
-        g_ts[kTsRes + 2 * task] = wsum;
-        g_ts[kTsRes + 2 * task + 1] = __builtin_amdgcn_s_memtime() - tk0;
+    // 8 slots per task: DMA-wait cycles, task cycles, start / end (100 MHz),
+    // HW_ID, XCC_ID, filter-fired groups, wave index in the workgroup
+    if (lane == 0 && 8 * task + 7 < 8 * 16384) {
+        uint64_t *o = g_ts + kTsRes + 8 * task;
+        o[0] = wsum;
+        o[1] = __builtin_amdgcn_s_memtime() - tk0;
+        o[2] = rt0;
+        o[3] = __builtin_amdgcn_s_memrealtime();
+        o[4] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+        o[5] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11));
+        o[6] = nrc;
+        o[7] = wave;
     }
 #endif
 }

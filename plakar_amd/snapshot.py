@@ -274,7 +274,9 @@ class BackupSession:
         _lib.check(_lib.lib().cdc_backup_new(int(dev), ctypes.byref(o), ctypes.byref(self._h)), "cdc_backup_new")
 
     def run(self, paths, keep_packfiles=True):
-        """Back up the files: (objects, packfiles, stats), as backup_files."""
+        """Back up the files: (objects, packfiles, stats), as backup_files.
+        A file that cannot be read has no object (None) and its status in
+        self.failed; the others are backed up."""
         import ctypes
         from . import _lib
         if not self._h:
@@ -282,24 +284,36 @@ class BackupSession:
         n = len(paths)
         arr = (ctypes.c_char_p * max(n, 1))(*[str(p).encode() for p in paths])
         objects = [None] * n
+        pending = {}  # file index -> chunks of its pieces so far (files larger than batch_bytes)
+        self.failed = {}  # file index -> status of the files that could not be read (recordError)
         packs = []
         errors = []
 
         def on_file(_ctx, fp):
             try:
                 f = fp.contents
+                i = int(f.index)
+                if f.status != 0:  # backupCtx.recordError (snapshot/backup.go:264-267): no object, the run goes on
+                    self.failed[i] = int(f.status)
+                    pending.pop(i, None)
+                    return
                 m = int(f.nchunks)
-                cuts = np.ctypeslib.as_array(ctypes.cast(f.cuts, ctypes.POINTER(ctypes.c_uint8)), (16 * m,)).view(
-                    np.dtype(_lib.CUT_DTYPE_FIELDS))
-                dg = np.ctypeslib.as_array(f.digests, (32 * m,))
-                hist = np.ctypeslib.as_array(f.hists, (256 * m,)).reshape(m, 256)
-                lens = cuts["length"].astype(np.int64)
-                ent = np.ctypeslib.as_array(f.entropy, (m,)).tolist()  # the device's entropy() per chunk
-                dist = hist / np.maximum(lens, 1)[:, None].astype(np.float64)
-                dg = dg.tobytes()
-                chunks = [hashing.Chunk(dg[32 * k:32 * k + 32], int(lens[k]), ent[k], dist[k]) for k in range(m)]
-                objects[int(f.index)] = Object(Checksum=bytes(f.checksum), Chunks=chunks,
-                                               Entropy=float(f.object_entropy))
+                chunks = pending.pop(i, [])
+                if m:
+                    cuts = np.ctypeslib.as_array(ctypes.cast(f.cuts, ctypes.POINTER(ctypes.c_uint8)),
+                                                 (16 * m,)).view(np.dtype(_lib.CUT_DTYPE_FIELDS))
+                    dg = np.ctypeslib.as_array(f.digests, (32 * m,))
+                    hist = np.ctypeslib.as_array(f.hists, (256 * m,)).reshape(m, 256)
+                    lens = cuts["length"].astype(np.int64)
+                    ent = np.ctypeslib.as_array(f.entropy, (m,)).tolist()  # the device's entropy() per chunk
+                    dist = hist / np.maximum(lens, 1)[:, None].astype(np.float64)
+                    dg = dg.tobytes()
+                    chunks += [hashing.Chunk(dg[32 * k:32 * k + 32], int(lens[k]), ent[k], dist[k])
+                               for k in range(m)]
+                if int(f.piece) + 1 < int(f.pieces):
+                    pending[i] = chunks
+                    return
+                objects[i] = Object(Checksum=bytes(f.checksum), Chunks=chunks, Entropy=float(f.object_entropy))
             except Exception as e:  # noqa: BLE001 - re-raised after the call
                 errors.append(e)
 

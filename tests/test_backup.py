@@ -97,12 +97,74 @@ def test_backup_files_known_digests_are_skipped(corpus):
     assert set(_blobs_of(packs3, KEY, True)) == every - some and st3["new_blobs"] == len(every - some)
 
 
-def test_backup_files_unreadable_path_fails_cleanly(tmp_path):
-    p = tmp_path / "ok"
-    p.write_bytes(b"x" * 100)
-    with pytest.raises(_lib.CdcError) as e:
-        snapshot.backup_files([str(p), str(tmp_path / "missing")])
-    assert e.value.status == _lib.CDC_E_IO
+def test_backup_files_unreadable_files_are_recorded_and_the_rest_backed_up(tmp_path):
+    """A missing path, a directory and a file that ends before its stat()
+    size each fail on their own (status CDC_E_IO, no object), as
+    backupCtx.recordError does (snapshot/backup.go:264-267); every other file
+    is backed up and packed."""
+    good = [random_bytes(200_000, 31).tobytes(), b"x" * 100, random_bytes(3 << 20, 32).tobytes()]
+    paths = []
+    for i, b in enumerate(good):
+        p = tmp_path / f"ok{i}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    (tmp_path / "adir").mkdir()
+    bad = [str(tmp_path / "missing"), str(tmp_path / "adir")]
+    # a sysfs attribute: stat() says 4096 bytes, a read returns fewer (a file that shrank)
+    short = next((q for q in ("/sys/kernel/mm/transparent_hugepage/enabled", "/sys/kernel/profiling")
+                  if __import__("os").path.exists(q)), None)
+    if short:
+        bad.append(short)
+    order = [paths[0], bad[0], paths[1], bad[1], paths[2]] + bad[2:]
+    with snapshot.BackupSession(key=KEY, batch_bytes=8 << 20, packers=2) as s:
+        objs, packs, st = s.run(order)
+        failed = dict(s.failed)
+    idx_bad = [order.index(b) for b in bad]
+    assert sorted(failed) == idx_bad and all(v == _lib.CDC_E_IO for v in failed.values())
+    assert all(objs[i] is None for i in idx_bad)
+    ref_objs = snapshot.chunkify_batch(good)
+    for p, r in zip(paths, ref_objs):
+        o = objs[order.index(p)]
+        assert o.Checksum == r.Checksum and [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks]
+    assert st["failed_files"] == len(bad) and st["files"] == len(order)
+    assert st["bytes"] == sum(len(b) for b in good)
+    assert set(_blobs_of(packs, KEY, True)) == {c.Checksum for o in objs if o for c in o.Chunks}
+
+
+def test_backup_files_larger_than_the_batch_go_in_pieces(tmp_path):
+    """Files many times batch_bytes are processed piece by piece, each piece
+    chunked from the previous one's carried chunk start: the same cut points,
+    digests, entropies and object checksum as the whole-file path, while the
+    per-slot arena stays within batch_bytes + Max (not the largest file)."""
+    files = [random_bytes(70 << 20, 41).tobytes(), random_bytes(1 << 20, 42).tobytes(),
+             low_entropy(40 << 20, 43).tobytes(), random_bytes(33 << 20, 44).tobytes()]
+    paths = []
+    for i, b in enumerate(files):
+        p = tmp_path / f"big{i}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    objs, packs, st = snapshot.backup_files(paths, key=KEY, batch_bytes=8 << 20, packers=3)
+    ref_objs = snapshot.chunkify_batch(files)
+    for i, (o, r) in enumerate(zip(objs, ref_objs)):
+        assert o.Checksum == r.Checksum == hashlib.sha256(files[i]).digest(), f"file {i}"
+        assert [c.Length for c in o.Chunks] == [c.Length for c in r.Chunks], f"file {i}"
+        assert [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks], f"file {i}"
+        assert [c.Entropy for c in o.Chunks] == [c.Entropy for c in r.Chunks], f"file {i}"
+        assert o.Entropy == r.Entropy, f"file {i}"
+    piece = max(8 << 20, 4 * (4 << 20))  # cdc_backup: pieces of max(batch_bytes, 4 Max)
+    assert st["pieces"] == sum(max(1, -(-len(b) // piece)) if len(b) > piece else 1 for b in files)
+    assert st["slot_arena_bytes"] <= piece + (4 << 20)
+    assert st["bytes"] == sum(len(b) for b in files) and st["failed_files"] == 0
+    assert set(_blobs_of(packs, KEY, True)) == {c.Checksum for o in objs for c in o.Chunks}
+
+
+def test_backup_stats_report_the_hardware_queues():
+    """cdc_backup_new records GPU_MAX_HW_QUEUES (0: unset, HIP's default of 4)
+    and whether the pipeline's streams share hardware queues."""
+    import os
+    _, _, st = snapshot.backup_files([])
+    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+    assert st["hw_queues"] == q and st["streams_serialised"] == (1 if q < 8 else 0)
 
 
 def test_backup_session_reused_across_runs(corpus, tmp_path):

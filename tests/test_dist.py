@@ -86,9 +86,20 @@ def test_bench_spawns_its_own_ranks(n):
     assert rc == 0, err[-2000:]
     assert line["n_gpus"] == n and line["selftest"]
     assert len(line["per_rank_elapsed_s"]) == n
+    # every rank checked its own cut lists (AND over ranks), rank 0 timed the CPU baseline
+    assert line["parity_vs_oracle"] is True
+    assert line["cpu_baseline"] is not None and line["cpu_baseline"]["value"] > 0
     # the max over ranks is the slowest rank's time (rank r sleeps (r + 1) * 10 ms)
     assert line["elapsed_max_s"] == max(line["per_rank_elapsed_s"])
     assert line["per_rank_elapsed_s"][-1] >= 0.01 * n
+
+
+def test_bench_parity_is_the_and_over_ranks():
+    """One rank whose cut lists differ from the oracle turns the line's
+    parity_vs_oracle false, whichever rank it is."""
+    rc, line, err = _run_bench(["--gpus", "2"], {"BENCH_CPU_SELFTEST": "1", "BENCH_SELFTEST_BAD_RANK": "1"})
+    assert rc == 0, err[-2000:]
+    assert line["parity_vs_oracle"] is False
 
 
 def test_bench_refuses_a_mismatched_launcher():

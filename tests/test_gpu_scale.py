@@ -106,13 +106,17 @@ def test_bench_spawns_two_ranks_on_one_gpu():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["BENCH_REHEARSE_ONE_GPU"] = "1"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--size-mib", "64", "--no-cpu-baseline", "--digest-reps", "0", "--encode-reps", "0", "--e2e-reps", "0"]
+           "--size-mib", "64", "--cpu-seconds", "1", "--cpu-threads", "1", "--digest-reps", "0", "--encode-reps",
+           "0", "--e2e-reps", "0"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     import json
     d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert d["n_gpus"] == 2 and len(d["config"]["per_rank_gibs"]) == 2, d
     assert d["config"]["global_bytes"] == 2 * d["config"]["bytes_per_gpu"]
+    # each rank's cut lists checked against the oracle (AND over ranks); the CPU baseline at N = 2
+    assert d["parity_vs_oracle"] is True, d
+    assert d["cpu_baseline"] is not None and d["cpu_baseline"]["value"] > 0, d
 
 
 def test_sequential_fallback_cost_1GiB(oracle):

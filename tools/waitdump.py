@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--timed", type=int, default=20)
     ap.add_argument("--workload", default="c1")
     ap.add_argument("--waits", action="store_true")
+    ap.add_argument("--save", default=None, help="write the per-task records (.npy)")
     args = ap.parse_args()
     import torch
 
@@ -55,14 +56,37 @@ def main():
     if args.waits:
         ts = np.zeros(K_SLOTS, dtype=np.uint64)
         assert L.cdc_debug_timestamps(ts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), K_SLOTS) == 0
-        r = ts[K_RES:K_RES + 8 * 16384].astype(np.int64).reshape(-1, 2)
+        r = ts[K_RES:K_RES + 8 * 16384].astype(np.int64).reshape(-1, 8)
         r = r[r[:, 1] > 0]
+        if args.save:
+            np.save(args.save, r)
         w, t = r[:, 0], r[:, 1]
         f = w / t
         print(f"  tasks {len(r)}: task cycles p50 {np.median(t):.0f} p90 {np.percentile(t, 90):.0f}; "
               f"DMA-wait cycles p50 {np.median(w):.0f}; wait share p10 {np.percentile(f, 10):.3f} "
               f"p50 {np.median(f):.3f} p90 {np.percentile(f, 90):.3f}")
-
+        hw = r[:, 4]
+        fields = {"wave_slot": hw & 0xF, "simd": (hw >> 4) & 3, "cu": (hw >> 8) & 0xF, "se": (hw >> 13) & 7,
+                  "xcc": r[:, 5] & 0xF, "wave": r[:, 7], "rechecks": np.minimum(r[:, 6] // 4, 8) * 4}
+        t0 = r[:, 2] - r[:, 2].min()
+        print(f"  start spread (10 ns): p50 {np.median(t0):.0f} p90 {np.percentile(t0, 90):.0f} "
+              f"max {t0.max()}; end p50 {np.median(r[:, 3] - r[:, 2].min()):.0f} max {(r[:, 3] - r[:, 2].min()).max()}")
+        for name, v in fields.items():
+            rows = []
+            for k in np.unique(v):
+                m = v == k
+                rows.append(f"{k}:{np.median(t[m]) / 1e3:.0f}/{np.percentile(t[m], 90) / 1e3:.0f}K(n{m.sum()})")
+            print(f"  by {name}: " + " ".join(rows))
+        # rank of the wave's start within its SIMD (by s_memrealtime) in its workgroup
+        cyc_by_rank = {}
+        key = (r[:, 5] & 0xF) * 4096 + ((hw >> 8) & 0xFF) * 8 + ((hw >> 4) & 3)
+        for k in np.unique(key):
+            idx = np.where(key == k)[0]
+            order = idx[np.argsort(r[idx, 2], kind="stable")]
+            for j, i in enumerate(order):
+                cyc_by_rank.setdefault(j, []).append(t[i])
+        print("  by start rank on its SIMD: " + " ".join(
+            f"{j}:{np.median(v) / 1e3:.0f}/{np.percentile(v, 90) / 1e3:.0f}K(n{len(v)})" for j, v in sorted(cyc_by_rank.items())))
 
 if __name__ == "__main__":
     main()
