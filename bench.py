@@ -27,6 +27,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s chunked (device-resident, cut-points out) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SHA_LANES = 256 * 2 * 128  # k_chunk_digest: resident SHA-256 lanes (2 workgroups of 2 x 64 round lanes per CU)
+SHA_BLOCK_S = 2.05e-6      # one 64-B block per lane: the round wave's ~905 VALU at one wave per SIMD
 GIB = float(1 << 30)
 
 WORKLOADS = {
@@ -562,6 +564,10 @@ def main():
                     help="threads of the multi-threaded CPU oracle leg (16 = the GPU box's CPU share; 1 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the per-rank oracle check after the timed region")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the roofline loop (--steps single-stream passes after --warmup ones; no timed "
+                         "pipelined region, no side legs): under rocprofv3 --kernel-trace --stats the k_scan "
+                         "average of the summary is the line's roofline.kernel_avg_ms")
     ap.add_argument("--backup-readers", type=int, default=16, help="c4b: reader threads (reads + object SHA-256)")
     ap.add_argument("--backup-packers", type=int, default=8, help="c4b: packer threads")
     ap.add_argument("--streams", type=int, default=2,
@@ -576,6 +582,9 @@ def main():
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="reps of the PCIe-inclusive host-buffer leg (0 = skip)")
     args = ap.parse_args()
+    if args.roofline_only:
+        args.digest_reps = args.encode_reps = args.e2e_reps = 0
+        args.no_cpu_baseline = True
     host_default = WORKLOADS[args.workload].get("host", False)
     if args.steps is None:
         args.steps = 5 if host_default else 200
@@ -711,28 +720,32 @@ def main():
             step_no[0] += 1
             batches[i].launch(streams[i])
 
+    timed_steps = 0 if args.roofline_only else args.steps
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    out = None
+    for _ in range(timed_steps):
         out = step()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     barrier()
+    if out is None and host_mode:
+        out = step()
     if post_step is not None:
         out = post_step(out)
     elapsed = reduce_max(dist, world, t1 - t0, dev)
     per_rank = gather_per_rank(dist, world, t1 - t0, dev)
-    value = world * per_rank_bytes * args.steps / elapsed / GIB
+    value = world * per_rank_bytes * timed_steps / elapsed / GIB if timed_steps else None
 
     # Roofline pass (after the timed region, not part of `value`): the scan
     # kernel's duration from hipEvents on its own launch stream, one pass at a
     # time (no other pass overlapping it), so it is the kernel's own time.
     L.cdc_profile_collect(None, None, None, None)
     L.cdc_profile_enable(1)
-    rsteps = max(5, min(args.steps, 50))
+    rsteps = args.steps if args.roofline_only else max(5, min(args.steps, 50))
     for _ in range(rsteps):
         if host_mode:
             chunkers.ChunkBuffers(host_bufs, opts)
@@ -837,7 +850,8 @@ def main():
                   "chunk_params": "FASTCDC min 65536 / normal 1048576 / max 4194304",
                   "gear": "placeholder (v0.0.8 table unavailable; see DESIGN.md)",
                   "parallelism": f"independent buffers, 1 rank per GPU x {world}, no collective",
-                  "per_rank_gibs": [round(per_rank_bytes * args.steps / e / GIB, 2) for e in per_rank],
+                  "per_rank_gibs": [round(per_rank_bytes * timed_steps / e / GIB, 2) if timed_steps else None
+                                    for e in per_rank],
                   "chunks_per_step": nchunks,
                   "cdc_env": cdc_env}
         if host_mode:
@@ -852,9 +866,10 @@ def main():
                                 "resolution kernels overlap the next pass's scan; roofline.pipeline_avg_ms is the "
                                 "single-pass latency (first kernel to cut lists final)")
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 2) if value is not None else None, "unit": "GiB/s",
+            "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "ms_per_step": round(elapsed / timed_steps * 1e3, 4) if timed_steps else None, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": ("synthetic (numpy PCG64 uniform bytes in host memory; no dataset)" if host_mode else
                      "synthetic (torch Philox uniform bytes generated on the GPU; no dataset)"),
@@ -868,6 +883,25 @@ def main():
         }
         if host_mode and wl.get("backup") and backup_stats[0]:
             bs = backup_stats[0]
+            # The leg's device bound is the per-chunk SHA-256 (k_chunk_digest,
+            # DESIGN.md 5.9), not the scan: its roofline is the SHA-256 issue
+            # ceiling, every resident SHA lane (256 CUs x 2 workgroups x 128)
+            # finishing a 64-B block per 2.05 us (one round wave per SIMD).
+            # achieved = bytes hashed per digest launch / the launch's average
+            # duration (digest stage events per batch: arena cuts + SHA-256 +
+            # histograms + entropy).
+            if bs.get("batches") and bs.get("digest_s"):
+                peak = SHA_LANES * 64 / SHA_BLOCK_S / 1e9
+                per = bs["digest_s"] / bs["batches"]
+                ach = bs["bytes"] / bs["batches"] / per / 1e9
+                line["roofline"] = dict(bound="issue", kernel="k_chunk_digest (per-chunk SHA-256 + histograms)",
+                                        achieved=round(ach, 1), peak=round(peak, 1), unit="GB/s",
+                                        frac=round(ach / peak, 4), traffic=None,
+                                        kernel_avg_ms=round(per * 1e3, 3),
+                                        algorithmic_bytes_per_launch=int(bs["bytes"] / bs["batches"]),
+                                        note="a launch lasts as long as its longest chunk's serial SHA-256 chain; "
+                                             "a 256-MiB batch holds ~2,400 chunks against 65,536 resident lanes",
+                                        scan=roofline)
             line["backup_stages"] = dict(
                 {k: (round(v, 4) if isinstance(v, float) else v) for k, v in bs.items()},
                 readers=args.backup_readers, packers=args.backup_packers,

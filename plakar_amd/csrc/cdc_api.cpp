@@ -686,17 +686,48 @@ int pipeline_device(int di, const cdc_opts *o, BatchSource &src)
         active[s] = true;
         return CDC_OK;
     };
+    // A failure inside the loop (an allocation of the host-side lists) hands
+    // every batch it holds back with the status, after the device is done
+    // with their buffers, and the worker goes on with the next batch: no
+    // caller waits for a batch that nobody finishes.
+    auto fail_inflight = [&](std::vector<HostBuf *> &cur_batch, int st) {
+        if (lock.owns_lock()) {
+            (void)hipStreamSynchronize(ctx->stream);
+            if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
+        }
+        for (int s = 0; s < 2; ++s)
+            if (active[s]) {
+                active[s] = false;
+                fail(fl[s], st);
+            }
+        if (!cur_batch.empty()) fail(cur_batch, st);
+    };
+    // The device lock is also released every kBatchesPerLock batches (the
+    // pipeline drained first), so cdc_chunk callers of the same device are not
+    // starved by a steady stream of collector batches.
+    constexpr int kBatchesPerLock = 16;
+    int held = 0;
     int cur = 0;
     for (;;) {
-        const bool busy = active[0] || active[1];
-        if (!busy && lock.owns_lock()) lock.unlock();  // drained: other callers may use the device
         std::vector<HostBuf *> batch;
+        try {
+        bool busy = active[0] || active[1];
+        if (busy && held >= kBatchesPerLock) {
+            harvest(cur ^ 1);  // the older group first
+            harvest(cur);
+            busy = false;
+        }
+        if (!busy && lock.owns_lock()) {  // drained: other callers may use the device
+            lock.unlock();
+            held = 0;
+        }
         if (!src.next(batch, !busy)) {
             if (!busy) return CDC_OK;  // the source is stopping
             harvest(active[cur] ? cur : cur ^ 1);  // the older group first (cur is the slot used next)
             continue;
         }
         if (batch.empty()) continue;
+        ++held;
         if (!lock.owns_lock()) {
             lock.lock();
             int st = hipSetDevice(ctx->device) == hipSuccess ? CDC_OK : CDC_E_DEVICE;
@@ -715,6 +746,11 @@ int pipeline_device(int di, const cdc_opts *o, BatchSource &src)
         if (st != CDC_OK) {
             fail(batch, st);
             harvest(s ^ 1);
+        }
+        } catch (const std::bad_alloc &) {
+            fail_inflight(batch, CDC_E_NOMEM);
+        } catch (...) {
+            fail_inflight(batch, CDC_E_DEVICE);
         }
     }
 }

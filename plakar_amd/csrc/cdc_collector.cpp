@@ -53,6 +53,7 @@ struct cdc_collector final : cdc::BatchSource {
     bool stop = false;
     uint64_t n_requests = 0, n_batches = 0;
     uint64_t callers = 0;  // threads inside cdc_collector_chunk
+    int live = 0;          // workers still serving the queue
     std::vector<std::thread> workers;
 
     bool closed(std::chrono::steady_clock::time_point now) const
@@ -129,6 +130,10 @@ struct cdc_collector final : cdc::BatchSource {
         } catch (...) {
             st = CDC_E_DEVICE;
         }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            --live;  // the last worker gone: new calls fail at once (cdc_collector_chunk)
+        }
         if (st != CDC_OK) fail_all(st);
     }
 };
@@ -148,6 +153,7 @@ int cdc_collector_new(const cdc_opts *opts, uint64_t batch_bytes, uint32_t max_w
     c->batch_bytes = batch_bytes ? batch_bytes : (256ull << 20);
     c->max_wait = std::chrono::microseconds(max_wait_us);
     try {
+        c->live = ndev;
         for (int d = 0; d < ndev; ++d) c->workers.emplace_back([c, d] { c->run(d); });
     } catch (...) {
         {
@@ -178,6 +184,7 @@ int cdc_collector_chunk(cdc_collector *c, const void *data, uint64_t len, cdc_cu
     r.cap = cap;
     std::unique_lock<std::mutex> lk(c->mu);
     if (c->stop) return CDC_E_INVALID;
+    if (c->live <= 0) return CDC_E_DEVICE;  // every worker failed: nobody would serve the call
     ++c->callers;
     try {
         if (c->queue.empty()) c->first_arrival = std::chrono::steady_clock::now();

@@ -217,6 +217,7 @@ constexpr uint32_t kTsClkN = kTsClk + 4 * kClkRecs;   // ring counter
 constexpr uint32_t kTsHw = kTsClkN + 1;               // per scan workgroup: XCC_ID << 32 | HW_ID (kDbgTs)
 constexpr uint32_t kTsSlots = kTsHw + 4096;
 constexpr uint32_t kDbgClk = 64;
+constexpr uint32_t kDbgNoJunctionHint = 128;  // k_walk: junction steps by plain next_node_skip() (A/B)
 __device__ uint64_t g_ts[kTsSlots];
 
 __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
@@ -572,6 +573,9 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     auto issue = [&](auto PC, uint32_t u) {
         constexpr uint32_t Q = decltype(PC)::value;  // u & 1: the half this DMA feeds
         const uint64_t adv = uint64_t(kStage) * (u - Q) + (Q ? half_step : 0ull);
+#ifdef CDC_DIAG_NO_DMA
+        return;  // build-time diagnostic only: no DMA (the slot keeps stale bytes), timing only
+#endif
         if (om0 + adv <= uint64_t(lim)) {
 #ifdef CDC_DIAG_L2
             // build-time diagnostic only: every DMA reads a 512-KiB window of
@@ -589,6 +593,11 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     };
     const char *rowp = s_lds + kGearLdsBytes + wave * kStageBytes + row * 128u;
     auto load_row = [&](uint4 (&first)[4], uint4 (&second)[4]) {
+#ifdef CDC_DIAG_NO_ROW
+        // build-time diagnostic only: no row reads (the registers keep stale bytes), timing only
+        asm volatile("" : "+v"(first[0].x), "+v"(second[0].x));
+        return;
+#endif
 #pragma unroll
         for (uint32_t g = 0; g < 4; ++g) first[g] = *reinterpret_cast<const uint4 *>(rowp + 16u * (g ^ swz));
 #pragma unroll
@@ -1183,52 +1192,82 @@ __device__ __forceinline__ uint32_t skip_exact(uint64_t &fp, const uint64_t (&g)
 // the exact test) or MaskL (kL = true: its exact window in the MaskS frame,
 // P.fm_ok).  kNoHit if none.  lo >= Min >= 64, so the warm-up of the first
 // block stays inside the buffer's first 16-byte block.
+//
+// Pipelined over blocks: a lane's 320 bytes of a block (64 B of warm-up + its
+// 256-B slice) are two register halves of 10 groups; while the lane rolls one
+// half of block b, the other half's buffer already takes its next bytes (the
+// second half of b, then the first half of b + 1, issued speculatively: a
+// block holds the first hit with probability ~0.4 on random data, and a
+// wasted prefetch costs only bandwidth).  Only a walk's first block waits for
+// its loads.  (Round 3's version loaded a whole block, then rolled it: every
+// block paid a full load latency.)
 template <bool kL>
 __device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo, uint64_t hi, uint64_t fz)
 {
+    static_assert(kSkipGroups == 20 && kSkipWarm == 64 && kSkipLane == 256, "two halves of 10 groups");
     const uint32_t lane = C.lane;
     const lds_char *tab = C.tab32;
     const uint32_t laneoff = C.laneoff32;
-    const uint64_t FZ = C.ub + fz, H = C.ub + hi, END = C.ub + C.len;
+    const uint64_t H = C.ub + hi, END = C.ub + C.len;
     const uint32_t vm = to_vgpr(kL ? P.fm_m : P.fs_hi);
     const uint32_t lws = P.fm_ws;
     const int32_t lo_off = int32_t(lane * kSkipLane);
-    uint64_t x = C.ub + lo;
-    while (x < H) {
-        const uint64_t A = x & ~15ull;
-        const uint64_t base = A - kSkipWarm;  // wave-uniform
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, END - base);
-        // this lane's tested range [tsr, ter) and the reset point, relative to base
-        const int32_t xr = int32_t(x - base);
-        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr);
-        const int32_t ter = int32_t(min<uint64_t>(uint64_t(lo_off) + kSkipWarm + kSkipLane, H - base));
-        const int32_t fzr = FZ >= base ? int32_t(FZ - base) : -1;
-        uint4 d[kSkipGroups];
+    const uint64_t x0 = C.ub + lo;
+    const uint64_t A0 = x0 & ~15ull, base0 = A0 - kSkipWarm;  // block b's lanes start at A0 + 16 KiB b
+    const uint32_t nblk = uint32_t((H - A0 + 64ull * kSkipLane - 1) / (64ull * kSkipLane));  // hi - lo <= Max
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base0, END - base0);  // reads past the buffer return 0
+    const int32_t xr0 = int32_t(x0 - base0);
+    const int32_t fzr0 = int32_t(int64_t(C.ub + fz) - int64_t(base0));  // <= xr0
+    constexpr uint32_t kHalf = kSkipGroups / 2;
+    uint4 h0[kHalf], h1[kHalf];
+    // Loads are unconditional (the waits below count them): past the last
+    // block a half is read from an offset beyond the resource's range, which
+    // returns zeros without a memory access.
+    auto load_half = [&](uint4 (&d)[kHalf], uint32_t blk, uint32_t half, bool real) {
+        const uint32_t o = real ? blk * 64u * kSkipLane + uint32_t(lo_off) + 16u * kHalf * half : 0xFFFFFE00u;
 #pragma unroll
-        for (uint32_t i = 0; i < kSkipGroups; ++i)
-            d[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo_off + int32_t(16 * i), 0, 0));
-        uint64_t gv[2][16];
+        for (uint32_t i = 0; i < kHalf; ++i)
+            d[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, int32_t(o + 16u * i), 0, 0));
+    };
+    load_half(h0, 0, 0, true);
+    load_half(h1, 0, 1, true);
+    // (the compiler's waits count the loads in issue order: group i waits for
+    // its own 16 bytes only, the younger loads stay in flight)
+    uint64_t gv[2][16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
+    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(h0[0], k >> 2), k));
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const int32_t bo = int32_t(b * 64u * kSkipLane);  // block b relative to block 0
+        // this lane's tested range [tsr, ter) and the reset point, relative to its block's base
+        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr0 - bo);
+        const int32_t ter = int32_t(min<int64_t>(int64_t(lo_off) + kSkipWarm + kSkipLane, int64_t(H - base0) - bo));
+        const int32_t fzr = fzr0 - bo;  // negative past block 0
+        const bool more = b + 1 < nblk;
         uint64_t fp = 0;
         uint32_t hit = ~0u;
 #pragma unroll
         for (uint32_t i = 0; i < kSkipGroups; ++i) {
+            // h0 (h1) is consumed once its last group's gathers were issued: it
+            // takes block b + 1's first (second) half
+            if (i == kHalf - 1) load_half(h0, b + 1, 0, more);
+            if (i == kSkipGroups - 1) load_half(h1, b + 1, 1, more);
             uint64_t (&cg)[16] = gv[i & 1];
             uint64_t (&ng)[16] = gv[(i + 1) & 1];
-            const uint4 nx = d[i + 1 < kSkipGroups ? i + 1 : i];
+            // the next group's bytes: block b + 1's first group after the last one
+            const uint4 nx = i + 1 < kHalf ? h0[i + 1] : i + 1 < kSkipGroups ? h1[i + 1 - kHalf] : h0[0];
+            const bool gnext = i + 1 < kSkipGroups || more;
             const uint64_t f0 = fp;
             uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
             for (int k = 0; k < 16; k += 2) {
                 const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
                 fp = (fp << 1) + cg[k];
-                if (i + 1 < kSkipGroups) ng[k] = lds_gear(tab, a0);
+                if (gnext) ng[k] = lds_gear(tab, a0);
                 const uint32_t k0 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
                                        : (uint32_t(fp >> 32) & vm);
                 const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
                 fp = (fp << 1) + cg[k + 1];
-                if (i + 1 < kSkipGroups) ng[k + 1] = lds_gear(tab, a1);
+                if (gnext) ng[k + 1] = lds_gear(tab, a1);
                 const uint32_t k1 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
                                        : (uint32_t(fp >> 32) & vm);
                 acc = umin3(acc, k0, k1);
@@ -1248,8 +1287,9 @@ __device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo,
         }
         ++C.blocks;
         const uint64_t m = __ballot(hit != ~0u);
-        if (m) return base + uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) - C.ub;
-        x = A + 64ull * kSkipLane;
+        if (m)
+            return base0 + uint64_t(bo) + uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) -
+                   C.ub;
     }
     return kNoHit;
 }
@@ -1293,6 +1333,64 @@ __device__ uint64_t next_node_skip(const WalkCtx &C, const DevParams &P, uint64_
         if (h != kNoHit) return h + P.cut_adj;
     }
     return clipped ? kUndet : p + n;
+}
+
+// A junction step of the skip walk (k_walk, phase B) from x, given the
+// speculative chain of the segment holding x (node i in lane i of cv, cns
+// nodes, cX the node after the last): the speculative walk already scanned
+// [p_k + Min, h] for its node p_k <= x < p_{k+1} = h + cut_adj and found no
+// full-window MaskS hit before h.  When h was such a hit (full window relative
+// to p_k, inside p_k's MaskS region) and lies at or past x's first
+// full-window position, it is x's next node too unless x's own truncated
+// window [x + Min, x + Min + W - 1) hits: one 49-byte check instead of a
+// scan.  When x is too close to p_{k+1} for that, only [x + Min, p_{k+1} + Min
+// + W - 1) is scanned: past it the speculative walk's next interval
+// [p_{k+1} + Min + W - 1, p_{k+2} - cut_adj) is hit-free, so without a hit the
+// answer is p_{k+2}.  Anything else takes the plain next_node_skip().
+__device__ uint64_t next_skip_junction(const WalkCtx &C, const DevParams &P, uint64_t x, uint64_t cv, uint32_t cns,
+                                       uint64_t cX)
+{
+    const uint64_t E = C.len, r = E - x;
+    const uint64_t m = __ballot(C.lane < cns && cv <= x);
+    if (r <= P.min_size || !m) return next_node_skip(C, P, x);
+    const int kk = 63 - int(__builtin_clzll(m));
+    const uint64_t pk = readlane64(cv, kk);
+    const uint64_t pk1 = kk + 1 < int(cns) ? readlane64(cv, kk + 1) : cX;
+    const uint64_t pk2 = kk + 2 < int(cns) ? readlane64(cv, kk + 2) : kk + 1 < int(cns) ? cX : kUndet;
+    // x's MaskS region [x + Min, s_end), as next_node_skip() bounds it
+    uint64_t norm = P.normal_size, lim;
+    if (C.final_) {
+        const uint64_t n = r >= P.max_size ? P.max_size : r;
+        if (r < P.max_size && r <= P.normal_size) norm = r;
+        lim = x + n;
+    } else {
+        lim = min(x + P.max_size, E);
+    }
+    const uint64_t s_end = min(x + norm, lim);
+    const uint64_t wm1 = P.win - 1;
+    // a node decided by a full-window MaskS hit of its predecessor q (not a
+    // truncated-window hit, not MaskL, not a forced or end-of-buffer cut)
+    auto full_hit_of = [&](uint64_t q, uint64_t nxt) {
+        return nxt != kUndet && nxt < E && nxt > q && nxt - P.cut_adj >= q + P.min_size + wm1 &&
+               nxt - P.cut_adj < q + P.normal_size;
+    };
+    if (!(x < pk1 && full_hit_of(pk, pk1))) return next_node_skip(C, P, x);
+    const uint64_t h = pk1 - P.cut_adj;
+    const uint64_t fz = x + P.min_size;
+    if (h >= fz + wm1 && h < s_end) {  // only x's truncated window is new
+        const uint32_t j = C.lane;
+        const uint64_t tpos = fz + j;
+        const uint32_t byte = (j + 1 < P.win && tpos < lim) ? as_space<const g_u8>(C.ub)[tpos] : 0u;
+        const uint64_t t = trunc_first_hit(C, P, fz, x + norm, lim, byte);
+        return t != kNoHit ? t + P.cut_adj : pk1;
+    }
+    const uint64_t stop = min(s_end, pk1 + P.min_size + wm1);
+    if (fz < stop) {
+        const uint64_t hh = skip_scan<false>(C, P, fz, stop, fz);
+        if (hh != kNoHit) return hh + P.cut_adj;
+    }
+    if (stop < s_end && full_hit_of(pk1, pk2) && pk2 - P.cut_adj < s_end) return pk2;
+    return next_node_skip(C, P, x);
 }
 
 template <bool kSkip>
@@ -2015,6 +2113,10 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 }
                 if (s != kGHard) {
                     nx = s;
+                } else if (kSkip && phase == 1 && !(B.debug & kDbgNoJunctionHint)) {
+                    nx = next_skip_junction(C, P, x, cv, cns, cX);
+                    ni = kGNone;
+                    ++exact;
                 } else {
                     nx = next_of<kSkip>(C, P, x);
                     ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
