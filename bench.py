@@ -112,15 +112,23 @@ def make_host_corpus(wl, rank, world):
 
 
 def e2e_host_rate(chunkers, opts, host_bufs, reps):
-    """PCIe-inclusive rate of the host-buffer path (cdc_chunk: pageable host
-    bytes -> pinned staging -> HBM -> kernels -> cut lists in host memory)."""
+    """PCIe-inclusive rate of the host-buffer path (cdc_chunk: host bytes ->
+    HBM -> kernels -> cut lists in host memory), from the MEDIAN call of
+    `reps` timed calls after a warm-up call (one call in ~10 was seen to take
+    5x the others from pinned memory on a 64-MiB buffer, which a 3-call mean
+    turned into "pinned slower than pageable"; tools/pinned_probe.py).
+    Returns (GiB/s of the median call, its seconds, the cut lists, per-call
+    seconds)."""
+    import statistics
     chunkers.ChunkBuffers(host_bufs, opts)  # warm-up: arenas, pinned staging
     total = sum(a.size for a in host_bufs)
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         res = chunkers.ChunkBuffers(host_bufs, opts)
-    el = time.perf_counter() - t0
-    return total * reps / el / GIB, el / reps, res
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return total / med / GIB, med, res, ts
 
 
 def load_traffic(workload):
@@ -570,6 +578,8 @@ def main():
                          "average of the summary is the line's roofline.kernel_avg_ms")
     ap.add_argument("--backup-readers", type=int, default=16, help="c4b: reader threads (reads + object SHA-256)")
     ap.add_argument("--backup-packers", type=int, default=8, help="c4b: packer threads")
+    ap.add_argument("--backup-batch-mib", type=int, default=512,
+                    help="c4b: bytes per device batch (MiB; 512 measured best of 256 / 512 / 1024, profiles/r04_c4b_batch.txt)")
     ap.add_argument("--streams", type=int, default=2,
                     help="device workloads: consecutive steps alternate over this many streams, each with its "
                          "own workspace, so one batch's resolution kernels overlap the next batch's scan")
@@ -579,8 +589,8 @@ def main():
                     help="reps of the per-chunk SHA-256 + histogram leg (SURVEY.md 8f; 0 = skip)")
     ap.add_argument("--digest-window", type=int, default=8,
                     help="passes per digest launch in the pipelined chunk + digest leg")
-    ap.add_argument("--e2e-reps", type=int, default=3,
-                    help="reps of the PCIe-inclusive host-buffer leg (0 = skip)")
+    ap.add_argument("--e2e-reps", type=int, default=9,
+                    help="timed calls of the PCIe-inclusive host-buffer leg, median reported (0 = skip)")
     args = ap.parse_args()
     if args.roofline_only:
         args.digest_reps = args.encode_reps = args.e2e_reps = 0
@@ -689,6 +699,7 @@ def main():
                 session_key = os.urandom(32)
                 session = snapshot.BackupSession(key=session_key, compression="LZ4", packers=args.backup_packers,
                                                  readers=args.backup_readers,
+                                                 batch_bytes=args.backup_batch_mib << 20,
                                                  dev=local)
 
                 def step():  # one whole backup of the share per step (an empty repository each time)
@@ -710,6 +721,13 @@ def main():
         nstreams = max(1, args.streams)
         batches = [device.DeviceBatch(bufs, opts, final=True, device=local) for _ in range(nstreams)]
         streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+        if os.environ.get("BENCH_TOUCH_STREAMS", "1") == "1":
+            # Stream setup, not a chunking pass: HIP binds a stream to a hardware
+            # queue on its first command (~7 ms), which otherwise lands between
+            # the first two warm-up passes (profiles/r03zz_driver_cmd_timeline.txt).
+            for st in streams:
+                torch.cuda.Event().record(st)
+                st.synchronize()
         batch = batches[0]
         per_rank_bytes = sum(t.numel() for t in bufs)
         nbufs = len(bufs)
@@ -816,21 +834,23 @@ def main():
         elif args.e2e_reps > 0 or not args.no_cpu_baseline:
             host = [t.cpu().numpy() for t in bufs[:1]]
             if args.e2e_reps > 0:
-                rate, sec, e2e_cuts = e2e_host_rate(chunkers, opts, host, args.e2e_reps)
+                rate, sec, e2e_cuts, ts = e2e_host_rate(chunkers, opts, host, args.e2e_reps)
                 dev_cuts = [c.cpu().numpy().astype(np.uint64) for c in cuts[:len(e2e_cuts)]]
                 same = all(a.shape == d.shape and bool((a == d).all()) for a, d in zip(e2e_cuts, dev_cuts))
                 e2e = dict(value=round(rate, 2), unit="GiB/s", ms_per_call=round(sec * 1e3, 2),
+                           ms_per_call_min_max=[round(min(ts) * 1e3, 2), round(max(ts) * 1e3, 2)],
                            path="cdc_chunk: pageable host -> H2D (runtime-staged) -> kernels -> D2H cut lists",
-                           sample=f"{len(host)} x {host[0].size / GIB:.3g} GiB, {args.e2e_reps} reps",
+                           sample=f"{len(host)} x {host[0].size / GIB:.3g} GiB, median of {args.e2e_reps} calls",
                            same_cuts_as_device_path=same)
                 # the same bytes from pinned host memory (north_star's "pinned hipMemcpyAsync" form)
                 pinned = [torch.empty(t.numel(), dtype=torch.uint8, pin_memory=True) for t in bufs[:1]]
                 for p, t in zip(pinned, bufs[:1]):
                     p.copy_(t)
                 hostp = [p.numpy() for p in pinned]
-                rate_p, sec_p, cuts_p = e2e_host_rate(chunkers, opts, hostp, args.e2e_reps)
+                rate_p, sec_p, cuts_p, ts_p = e2e_host_rate(chunkers, opts, hostp, args.e2e_reps)
                 same_p = all(a.shape == d.shape and bool((a == d).all()) for a, d in zip(cuts_p, dev_cuts))
                 e2e["pinned"] = dict(value=round(rate_p, 2), unit="GiB/s", ms_per_call=round(sec_p * 1e3, 2),
+                                     ms_per_call_min_max=[round(min(ts_p) * 1e3, 2), round(max(ts_p) * 1e3, 2)],
                                      path="cdc_chunk: pinned host -> H2D (direct DMA) -> kernels -> D2H cut lists",
                                      same_cuts_as_device_path=same_p)
                 del hostp, pinned
@@ -904,7 +924,7 @@ def main():
                                         scan=roofline)
             line["backup_stages"] = dict(
                 {k: (round(v, 4) if isinstance(v, float) else v) for k, v in bs.items()},
-                readers=args.backup_readers, packers=args.backup_packers,
+                readers=args.backup_readers, packers=args.backup_packers, batch_mib=args.backup_batch_mib,
                 GPU_MAX_HW_QUEUES=os.environ.get("GPU_MAX_HW_QUEUES"),
                 GPU_MAX_HW_QUEUES_given=os.environ.get("BENCH_GPU_MAX_HW_QUEUES_GIVEN") or None,
                 note="per step (the last one): seconds per stage; read_s / objhash_s / pack_s are thread times "

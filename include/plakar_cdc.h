@@ -208,7 +208,9 @@ void cdc_packer_free(cdc_packer *p);
  * threads append the blobs to their own packfiles and hand each one, at
  * Size() > packfile_max (0: 20 MiB) and at the end, to on_pack (PutPackfile;
  * calls are serialised, from packer threads).  on_file is called once per
- * file, in order, from one library thread (the calling thread meanwhile
+ * file, largest files first (the order the pipeline processes them: a large
+ * file's object hash is a long serial chain), from one library thread (the
+ * calling thread meanwhile
  * drives the next batches through the device), with pointers valid during the
  * call only; chunk entropies come from the device (cdc_chunk_entropy_device_async).
  * An empty file is one empty chunk (backup.go:631-635); a file shorter than

@@ -351,6 +351,26 @@ int plan(Run &R, uint64_t &arena_cap, uint64_t &cuts_cap, uint64_t &ws_cap, uint
             R.units.push_back(u);
         }
     }
+    // Largest files first: a file's object SHA-256 is one serial chain on a
+    // host core (a 128-MiB file ~64 ms) and a slot is released only once
+    // every hash of its batch is done, so a large file late in the run held
+    // the device idle behind its hash (profiles/r03_c4b_timeline.txt: gaps of
+    // 15-70 ms).  Pieces of one file stay consecutive; callbacks come in this
+    // processing order (each names its file).
+    {
+        std::vector<uint32_t> first(size_t(R.n) + 1, 0);  // units of file i: [first[i], first[i + 1])
+        for (size_t u = 0; u < R.units.size(); ++u) first[R.units[u].file + 1] = uint32_t(u + 1);
+        for (int i = 0; i < R.n; ++i) first[size_t(i) + 1] = std::max(first[size_t(i) + 1], first[size_t(i)]);
+        std::vector<uint32_t> ord(size_t(R.n));
+        for (int i = 0; i < R.n; ++i) ord[size_t(i)] = uint32_t(i);
+        std::stable_sort(ord.begin(), ord.end(),
+                         [&](uint32_t a, uint32_t b) { return R.files[a].size > R.files[b].size; });
+        std::vector<Unit> sorted;
+        sorted.reserve(R.units.size());
+        for (uint32_t i : ord)
+            for (uint32_t u = first[i]; u < first[i + 1]; ++u) sorted.push_back(R.units[u]);
+        R.units.swap(sorted);
+    }
     R.batch_of.resize(R.units.size());
     Batch cur{0, 0, 0, 0};
     for (uint32_t k = 0; k < uint32_t(R.units.size()); ++k) {

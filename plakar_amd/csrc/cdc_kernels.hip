@@ -1201,73 +1201,54 @@ __device__ __forceinline__ uint32_t skip_exact(uint64_t &fp, const uint64_t (&g)
 // wasted prefetch costs only bandwidth).  Only a walk's first block waits for
 // its loads.  (Round 3's version loaded a whole block, then rolled it: every
 // block paid a full load latency.)
+#ifdef CDC_SKIP_V3
+// build-time A/B only: round 3's skip_scan (load a block, then roll it)
 template <bool kL>
 __device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo, uint64_t hi, uint64_t fz)
 {
-    static_assert(kSkipGroups == 20 && kSkipWarm == 64 && kSkipLane == 256, "two halves of 10 groups");
     const uint32_t lane = C.lane;
     const lds_char *tab = C.tab32;
     const uint32_t laneoff = C.laneoff32;
-    const uint64_t H = C.ub + hi, END = C.ub + C.len;
+    const uint64_t FZ = C.ub + fz, H = C.ub + hi, END = C.ub + C.len;
     const uint32_t vm = to_vgpr(kL ? P.fm_m : P.fs_hi);
     const uint32_t lws = P.fm_ws;
     const int32_t lo_off = int32_t(lane * kSkipLane);
-    const uint64_t x0 = C.ub + lo;
-    const uint64_t A0 = x0 & ~15ull, base0 = A0 - kSkipWarm;  // block b's lanes start at A0 + 16 KiB b
-    const uint32_t nblk = uint32_t((H - A0 + 64ull * kSkipLane - 1) / (64ull * kSkipLane));  // hi - lo <= Max
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base0, END - base0);  // reads past the buffer return 0
-    const int32_t xr0 = int32_t(x0 - base0);
-    const int32_t fzr0 = int32_t(int64_t(C.ub + fz) - int64_t(base0));  // <= xr0
-    constexpr uint32_t kHalf = kSkipGroups / 2;
-    uint4 h0[kHalf], h1[kHalf];
-    // Loads are unconditional (the waits below count them): past the last
-    // block a half is read from an offset beyond the resource's range, which
-    // returns zeros without a memory access.
-    auto load_half = [&](uint4 (&d)[kHalf], uint32_t blk, uint32_t half, bool real) {
-        const uint32_t o = real ? blk * 64u * kSkipLane + uint32_t(lo_off) + 16u * kHalf * half : 0xFFFFFE00u;
+    uint64_t x = C.ub + lo;
+    while (x < H) {
+        const uint64_t A = x & ~15ull;
+        const uint64_t base = A - kSkipWarm;  // wave-uniform
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, END - base);
+        // this lane's tested range [tsr, ter) and the reset point, relative to base
+        const int32_t xr = int32_t(x - base);
+        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr);
+        const int32_t ter = int32_t(min<uint64_t>(uint64_t(lo_off) + kSkipWarm + kSkipLane, H - base));
+        const int32_t fzr = FZ >= base ? int32_t(FZ - base) : -1;
+        uint4 d[kSkipGroups];
 #pragma unroll
-        for (uint32_t i = 0; i < kHalf; ++i)
-            d[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, int32_t(o + 16u * i), 0, 0));
-    };
-    load_half(h0, 0, 0, true);
-    load_half(h1, 0, 1, true);
-    // (the compiler's waits count the loads in issue order: group i waits for
-    // its own 16 bytes only, the younger loads stay in flight)
-    uint64_t gv[2][16];
+        for (uint32_t i = 0; i < kSkipGroups; ++i)
+            d[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo_off + int32_t(16 * i), 0, 0));
+        uint64_t gv[2][16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(h0[0], k >> 2), k));
-    for (uint32_t b = 0; b < nblk; ++b) {
-        const int32_t bo = int32_t(b * 64u * kSkipLane);  // block b relative to block 0
-        // this lane's tested range [tsr, ter) and the reset point, relative to its block's base
-        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr0 - bo);
-        const int32_t ter = int32_t(min<int64_t>(int64_t(lo_off) + kSkipWarm + kSkipLane, int64_t(H - base0) - bo));
-        const int32_t fzr = fzr0 - bo;  // negative past block 0
-        const bool more = b + 1 < nblk;
+        for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
         uint64_t fp = 0;
         uint32_t hit = ~0u;
 #pragma unroll
         for (uint32_t i = 0; i < kSkipGroups; ++i) {
-            // h0 (h1) is consumed once its last group's gathers were issued: it
-            // takes block b + 1's first (second) half
-            if (i == kHalf - 1) load_half(h0, b + 1, 0, more);
-            if (i == kSkipGroups - 1) load_half(h1, b + 1, 1, more);
             uint64_t (&cg)[16] = gv[i & 1];
             uint64_t (&ng)[16] = gv[(i + 1) & 1];
-            // the next group's bytes: block b + 1's first group after the last one
-            const uint4 nx = i + 1 < kHalf ? h0[i + 1] : i + 1 < kSkipGroups ? h1[i + 1 - kHalf] : h0[0];
-            const bool gnext = i + 1 < kSkipGroups || more;
+            const uint4 nx = d[i + 1 < kSkipGroups ? i + 1 : i];
             const uint64_t f0 = fp;
             uint32_t acc = 0xFFFFFFFFu;
 #pragma unroll
             for (int k = 0; k < 16; k += 2) {
                 const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
                 fp = (fp << 1) + cg[k];
-                if (gnext) ng[k] = lds_gear(tab, a0);
+                if (i + 1 < kSkipGroups) ng[k] = lds_gear(tab, a0);
                 const uint32_t k0 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
                                        : (uint32_t(fp >> 32) & vm);
                 const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
                 fp = (fp << 1) + cg[k + 1];
-                if (gnext) ng[k + 1] = lds_gear(tab, a1);
+                if (i + 1 < kSkipGroups) ng[k + 1] = lds_gear(tab, a1);
                 const uint32_t k1 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
                                        : (uint32_t(fp >> 32) & vm);
                 acc = umin3(acc, k0, k1);
@@ -1287,12 +1268,139 @@ __device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo,
         }
         ++C.blocks;
         const uint64_t m = __ballot(hit != ~0u);
-        if (m)
-            return base0 + uint64_t(bo) + uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) -
-                   C.ub;
+        if (m) return base + uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) - C.ub;
+        x = A + 64ull * kSkipLane;
     }
     return kNoHit;
 }
+
+#else
+// First position in [lo, hi) (buffer-relative) whose fingerprint, reset to 0
+// at fz <= lo, hits: MaskS (kL = false: the hi-dword filter of k_scan, then
+// the exact test) or MaskL (kL = true: its exact window in the MaskS frame,
+// P.fm_ok).  kNoHit if none.  lo >= Min >= 64, so the warm-up of the first
+// block stays inside the buffer's first 16-byte block.
+//
+// Pipelined: a lane's 320 bytes of a block (64 B of warm-up + its 256-B
+// slice) are two halves of 10 groups.  The loop runs over halves; while the
+// lane rolls half h (cur), half h + 1 is already in registers or in flight
+// (nxt), and at the end of half h the loads of half h + 2 are issued into
+// cur's registers (the two arrays then swap: 40 moves per half).  Half h + 2
+// of the next block is read speculatively: a block holds the first hit with
+// probability ~0.4 on random data, and a wasted prefetch costs only
+// bandwidth.  Only a walk's first half waits for its loads.  (Round 3's
+// version loaded a whole block, then rolled it: every block paid a full load
+// latency.  A fully unrolled two-half body spilled: the register allocator
+// could not fit the 20 inlined rechecks beside 80 VGPRs of data.)
+template <bool kL>
+__device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo, uint64_t hi, uint64_t fz)
+{
+    static_assert(kSkipGroups == 20 && kSkipWarm == 64 && kSkipLane == 256, "two halves of 10 groups");
+    constexpr uint32_t kHalf = kSkipGroups / 2;
+    const uint32_t lane = C.lane;
+    const lds_char *tab = C.tab32;
+    const uint32_t laneoff = C.laneoff32;
+    const uint64_t H = C.ub + hi, END = C.ub + C.len;
+    const uint32_t vm = to_vgpr(kL ? P.fm_m : P.fs_hi);
+    const uint32_t lws = P.fm_ws;
+    const int32_t lo_off = int32_t(lane * kSkipLane);
+    const uint64_t x0 = C.ub + lo;
+    const uint64_t A0 = x0 & ~15ull, base0 = A0 - kSkipWarm;  // block b's lanes start at A0 + 16 KiB b
+    const uint32_t nblk = uint32_t((H - A0 + 64ull * kSkipLane - 1) / (64ull * kSkipLane));  // hi - lo <= Max
+    const uint32_t nhalf = 2 * nblk;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base0, END - base0);  // reads past the buffer return 0
+    const int32_t xr0 = int32_t(x0 - base0);
+    const int32_t fzr0 = int32_t(int64_t(C.ub + fz) - int64_t(base0));  // <= xr0
+    // Half hh's 10 loads (unconditional, so the waits count them: past the
+    // last half the offset lies beyond the resource's range, which returns
+    // zeros without a memory access).  The scheduling barriers keep them
+    // together at this point of the program.
+    auto load_half = [&](uint4 (&d)[kHalf], uint32_t hh) {
+        const uint32_t o = hh < nhalf ? (hh >> 1) * 64u * kSkipLane + uint32_t(lo_off) + 16u * kHalf * (hh & 1u)
+                                      : 0xFFFFFE00u;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (uint32_t i = 0; i < kHalf; ++i) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, int32_t(o + 16u * i), 0, 0);
+            d[i] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    uint4 cur[kHalf], nxt[kHalf];
+    load_half(cur, 0);
+    load_half(nxt, 1);
+    // (the compiler's waits count the loads in issue order: a group waits for
+    // its own 16 bytes only, the younger loads stay in flight)
+    uint64_t gv[2][16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(cur[0], k >> 2), k));
+    uint64_t fp = 0;
+    uint32_t hit = ~0u;
+    for (uint32_t h = 0; h < nhalf; ++h) {
+        const uint32_t b = h >> 1;
+        const int32_t bo = int32_t(b * 64u * kSkipLane);  // block b relative to block 0
+        // this lane's tested range [tsr, ter) and the reset point, relative to its block's base
+        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr0 - bo);
+        const int32_t ter = int32_t(min<int64_t>(int64_t(lo_off) + kSkipWarm + kSkipLane, int64_t(H - base0) - bo));
+        const int32_t fzr = fzr0 - bo;  // negative past block 0
+        const int32_t g0 = int32_t(kHalf * (h & 1u));  // this half's first group in the lane's slice
+        if ((h & 1u) == 0) fp = 0;  // a block starts a lane's warm-up
+#pragma unroll
+        for (uint32_t i = 0; i < kHalf; ++i) {
+            uint64_t (&cg)[16] = gv[i & 1];
+            uint64_t (&ng)[16] = gv[(i + 1) & 1];
+            // the next group's bytes (the next half's first group after the last one;
+            // past the last half they are zeros: harmless gathers)
+            const uint4 nx = i + 1 < kHalf ? cur[i + 1] : nxt[0];
+            const uint64_t f0 = fp;
+            uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < 16; k += 2) {
+                const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
+                fp = (fp << 1) + cg[k];
+                ng[k] = lds_gear(tab, a0);
+                const uint32_t k0 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
+                                       : (uint32_t(fp >> 32) & vm);
+                const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
+                fp = (fp << 1) + cg[k + 1];
+                ng[k + 1] = lds_gear(tab, a1);
+                const uint32_t k1 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
+                                       : (uint32_t(fp >> 32) & vm);
+                acc = umin3(acc, k0, k1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const int32_t gr = lo_off + 16 * (g0 + int32_t(i));
+            bool chk = acc == 0 && gr + 16 > tsr && gr < ter;
+            if (g0 == 0 && i * 16 <= kSkipWarm) {  // the groups that can lie before the reset point
+                if (gr + 16 <= fzr) fp = 0;
+                chk = chk || (gr < fzr && gr + 16 > fzr);
+            }
+            if (chk && hit == ~0u) [[unlikely]] {
+                uint64_t f = f0;
+                hit = skip_exact<kL>(f, cg, gr, tsr, ter, fzr, P);
+                fp = f;
+            }
+        }
+        // the two halves swap; half h + 2 goes into the registers of half h
+#pragma unroll
+        for (uint32_t i = 0; i < kHalf; ++i) {
+            const uint4 t = cur[i];
+            cur[i] = nxt[i];
+            nxt[i] = t;
+        }
+        load_half(nxt, h + 2);
+        if (h & 1u) {  // a block ends: the wave's first hit, if any
+            ++C.blocks;
+            const uint64_t m = __ballot(hit != ~0u);
+            if (m)
+                return base0 + uint64_t(bo) +
+                       uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) - C.ub;
+        }
+    }
+    return kNoHit;
+}
+
+#endif  // CDC_SKIP_V3
 
 // next_node() from the bytes alone (k_walk): the same window rules, every
 // candidate found by skip_scan (the truncated window included: skip_scan

@@ -2,7 +2,7 @@
 # skip walk (CDC_WALK_MODE=2): parity suite, then the driver's command and the warm default, walk vs full scan.
 O=gpurun_out/${1:-r04walk}; mkdir -p $O
 export PYTHONUNBUFFERED=1
-CDC_WALK_MODE=2 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest_walk.txt 2>&1; rc=$?
+CDC_WALK_MODE=2 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -q -m gpu --timeout 200 --timeout-method thread --deselect tests/test_gpu_parity.py::test_maskl_adaptive_follows_the_data > $O/pytest_walk.txt 2>&1; rc=$?
 tail -3 $O/pytest_walk.txt
 [ $rc -eq 0 ] || exit $rc
 FAST="--no-cpu-baseline --digest-reps 0 --encode-reps 0 --e2e-reps 0"
