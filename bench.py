@@ -721,13 +721,6 @@ def main():
         nstreams = max(1, args.streams)
         batches = [device.DeviceBatch(bufs, opts, final=True, device=local) for _ in range(nstreams)]
         streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
-        if os.environ.get("BENCH_TOUCH_STREAMS", "1") == "1":
-            # Stream setup, not a chunking pass: HIP binds a stream to a hardware
-            # queue on its first command (~7 ms), which otherwise lands between
-            # the first two warm-up passes (profiles/r03zz_driver_cmd_timeline.txt).
-            for st in streams:
-                torch.cuda.Event().record(st)
-                st.synchronize()
         batch = batches[0]
         per_rank_bytes = sum(t.numel() for t in bufs)
         nbufs = len(bufs)

@@ -288,6 +288,15 @@ struct Blob {
     int slot;
 };
 
+// Encode of one batch's new chunks, handed from the calling thread to the
+// encoder thread once the batch is deduplicated.
+struct EncJob {
+    size_t k;
+    std::vector<uint64_t> off, len;
+    std::vector<Digest> sum;
+    uint64_t bound;
+};
+
 struct Run {
     cdc_backup *B;
     const cdc_backup_opts &o;
@@ -305,6 +314,8 @@ struct Run {
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
     bool stop_packers = false;
+    std::deque<EncJob> enc_q;  // guarded by mu
+    bool stop_encoder = false;
     size_t devices_done = 0;  // batches through finish_device (callbacks may start)
     size_t cuts = 0, digs = 0;  // batches whose stage A / stage B is enqueued (the calling thread's)
     std::deque<Blob> queue;
@@ -761,37 +772,17 @@ int finish_device(Run &R, size_t k)
     }
     const uint32_t nb = uint32_t(enc_off.size());
     const bool encode = nb && (R.o.compress || R.o.key);
-    std::vector<uint64_t> oo(nb + 1, 0);
-    double enc_s = 0, d2h_enc_s = 0;
-    if (encode) {
-        if ((st = grow_dev(s.d_enc, s.enc_cap, enc_bound)) != CDC_OK) return st;
-        std::vector<uint8_t> rnd;
-        if (R.o.key) {
-            rnd.resize(56ull * nb);
-            if ((st = random_bytes(rnd.data(), rnd.size())) != CDC_OK) return st;
-        }
-        const auto e0 = Clock::now();
-        st = cdc_encode_device(R.B->device, s.d_in, enc_off.data(), enc_len.data(), nb, R.o.compress, R.o.key,
-                               R.o.key ? rnd.data() : nullptr, s.d_enc, s.enc_cap, oo.data(), R.B->stream[kE]);
-        if (st != CDC_OK) return st;
-        const auto e1 = Clock::now();
-        if (oo[nb] > s.henc_cap || !s.h_enc) {
-            const uint64_t want = std::max<uint64_t>(oo[nb], s.enc_cap);
-            if ((st = grow_host(s.h_enc, want, 0)) != CDC_OK) return st;
-            s.henc_cap = want;
-        }
-        HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, R.B->stream[kE]));
-        HIPOK(hipEventRecord(s.ev_enc, R.B->stream[kE]));
-        if ((st = wait_pumping(R, s.ev_enc, k)) != CDC_OK) return st;
-        enc_s = secs(e0, e1);
-        d2h_enc_s = secs(e1, Clock::now());
-    }
     {
+        // The new chunks go to the encoder thread (Encode, then the encoded
+        // blobs back, then the packers), so this thread goes on driving the
+        // next batches instead of waiting out Encode; the slot stays held
+        // until its blobs are packed.
         std::lock_guard<std::mutex> lk(R.mu);
-        for (uint32_t q = 0; q < nb; ++q) {
-            const uint8_t *p = encode ? s.h_enc + oo[q] : s.h_arena + enc_off[q];
-            const uint64_t len = encode ? oo[q + 1] - oo[q] : enc_len[q];
-            R.queue.push_back(Blob{enc_sum[q], p, len, int(k % kSlots)});
+        if (encode) {
+            R.enc_q.push_back(EncJob{k, std::move(enc_off), std::move(enc_len), std::move(enc_sum), enc_bound});
+        } else {
+            for (uint32_t q = 0; q < nb; ++q)
+                R.queue.push_back(Blob{enc_sum[q], s.h_arena + enc_off[q], enc_len[q], int(k % kSlots)});
         }
         s.pending += nb;
     }
@@ -805,14 +796,82 @@ int finish_device(Run &R, size_t k)
     R.st.chunks += nchunks;
     R.st.new_blobs += nb;
     R.st.new_bytes += new_bytes;
-    R.st.encoded_bytes += encode ? oo[nb] : new_bytes;
+    if (!encode) R.st.encoded_bytes += new_bytes;
     R.st.h2d_s += t[0] * 1e-3;
     R.st.chunk_s += t[1] * 1e-3;
     R.st.digest_s += t[2] * 1e-3;
-    R.st.d2h_s += t[3] * 1e-3 + d2h_enc_s;
-    R.st.encode_s += enc_s;
+    R.st.d2h_s += t[3] * 1e-3;
     R.st.device_s += s.t_enq + secs(w0, Clock::now());
     return CDC_OK;
+}
+
+// The encoder thread: each batch's new chunks through Encode (LZ4 frame +
+// AES-256-GCM on the device, stream E), the encoded blobs back to pinned
+// memory, then to the packers; batches in order.
+int encode_job(Run &R, EncJob &J)
+{
+    Slot &s = R.B->slot[J.k % kSlots];
+    const uint32_t nb = uint32_t(J.off.size());
+    int st;
+    if ((st = grow_dev(s.d_enc, s.enc_cap, J.bound)) != CDC_OK) return st;
+    std::vector<uint8_t> rnd;
+    if (R.o.key) {
+        rnd.resize(56ull * nb);
+        if ((st = random_bytes(rnd.data(), rnd.size())) != CDC_OK) return st;
+    }
+    std::vector<uint64_t> oo(nb + 1, 0);
+    const auto e0 = Clock::now();
+    st = cdc_encode_device(R.B->device, s.d_in, J.off.data(), J.len.data(), nb, R.o.compress, R.o.key,
+                           R.o.key ? rnd.data() : nullptr, s.d_enc, s.enc_cap, oo.data(), R.B->stream[kE]);
+    if (st != CDC_OK) return st;
+    const auto e1 = Clock::now();
+    if (oo[nb] > s.henc_cap || !s.h_enc) {
+        const uint64_t want = std::max<uint64_t>(oo[nb], s.enc_cap);
+        if ((st = grow_host(s.h_enc, want, 0)) != CDC_OK) return st;
+        s.henc_cap = want;
+    }
+    HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, R.B->stream[kE]));
+    HIPOK(hipStreamSynchronize(R.B->stream[kE]));
+    const auto e2 = Clock::now();
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        for (uint32_t q = 0; q < nb; ++q)
+            R.queue.push_back(Blob{J.sum[q], s.h_enc + oo[q], oo[q + 1] - oo[q], int(J.k % kSlots)});
+    }
+    R.cv.notify_all();
+    std::lock_guard<std::mutex> lk(R.stat_mu);
+    R.st.encoded_bytes += oo[nb];
+    R.st.encode_s += secs(e0, e1);
+    R.st.d2h_s += secs(e1, e2);
+    return CDC_OK;
+}
+
+void encoder_main(Run &R)
+{
+    if (hipSetDevice(R.B->device) != hipSuccess) {
+        R.fail(CDC_E_DEVICE);
+        return;
+    }
+    for (;;) {
+        EncJob J;
+        {
+            std::unique_lock<std::mutex> lk(R.mu);
+            R.cv.wait(lk, [&] { return !R.enc_q.empty() || R.stop_encoder || R.status.load() != CDC_OK; });
+            if (R.enc_q.empty() || R.status.load() != CDC_OK) return;
+            J = std::move(R.enc_q.front());
+            R.enc_q.pop_front();
+        }
+        int st;
+        try {
+            st = encode_job(R, J);
+        } catch (const std::bad_alloc &) {
+            st = CDC_E_NOMEM;
+        }
+        if (st != CDC_OK) {
+            R.fail(st);
+            return;
+        }
+    }
 }
 
 // Batch k's per-file callbacks (the Object's fields), on the callback thread
@@ -998,7 +1057,7 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
     R.ctx = ctx;
     int st = CDC_OK;
     std::vector<std::thread> readers, packers;
-    std::thread callbacks;
+    std::thread callbacks, encoder;
     try {
         uint64_t arena = 0, ncuts = 0, ws = 0, nfiles = 0;
         st = plan(R, arena, ncuts, ws, nfiles);
@@ -1026,6 +1085,7 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
             const int nr = std::max(1, R.o.readers ? R.o.readers : 8);
             for (int r = 0; r < nr; ++r) readers.emplace_back([&R] { reader_main(R); });
             callbacks = std::thread([&R] { callback_main(R); });
+            encoder = std::thread([&R] { encoder_main(R); });
             for (int p = 0; p < np; ++p) {
                 cdc_packer *pk = B->packers[size_t(p)];
                 packers.emplace_back([&R, pk] { packer_main(R, pk); });
@@ -1053,6 +1113,12 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
                 }
                 R.cv.notify_all();
             }
+            {  // every batch is handed over: the encoder drains its queue and stops
+                std::lock_guard<std::mutex> lk(R.mu);
+                R.stop_encoder = true;
+            }
+            R.cv.notify_all();
+            if (encoder.joinable()) encoder.join();
             if (st == CDC_OK && callbacks.joinable()) {
                 callbacks.join();  // the last slots are released by the callbacks
                 st = R.status.load();
@@ -1070,6 +1136,14 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
     } catch (...) {
         st = CDC_E_DEVICE;
         R.fail(st);
+    }
+    if (encoder.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(R.mu);
+            R.stop_encoder = true;
+        }
+        R.cv.notify_all();
+        encoder.join();
     }
     if (callbacks.joinable()) callbacks.join();
     for (auto &t : readers) t.join();
