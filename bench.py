@@ -775,7 +775,9 @@ def main():
     else:
         cuts, res = batch.results()
         nchunks = int(res[:, 0].sum())
-        for other in batches[1:]:  # every stream's batch produced the same cut lists
+        for i, other in enumerate(batches[1:], 1):  # every stream's batch produced the same cut lists
+            if step_no[0] <= i:  # never launched (--roofline-only without warmup: only batch 0 runs)
+                continue
             oc, _ = other.results()
             assert all(a.shape == b.shape and bool((a == b).all()) for a, b in zip(cuts, oc)), \
                 "pipelined batches disagree"

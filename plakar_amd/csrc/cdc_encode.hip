@@ -1120,8 +1120,18 @@ __global__ __launch_bounds__(kPowWaves * 64) void k_blob_pows(const Batch B)
     }
 }
 
+// Raw buffer resource over [base, base + bytes): reads past the end return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gcm_rsrc(uint64_t base, uint64_t bytes)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(base));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(base >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(uint32_t(bytes));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, int(n), 0x00020000);
+}
+
 constexpr uint32_t kGcmWaves = 12;  // one workgroup per CU (LDS: the 64-KiB table), three waves per SIMD
 
+#ifdef GCM_V1
 // LDS of a GCM workgroup.  The T-table in 64 copies, entry e of copy c at
 // byte 256 e + 4 c: lane l reads copy l, so its address is ONE v_perm of the
 // state word and the lane's offset (byte e in bits 8-15, 4 l in bits 0-7), and
@@ -1138,6 +1148,26 @@ struct GcmLds {
         uint4 stage[128];
     } w[kGcmWaves];
 };
+#else
+// LDS of a GCM workgroup.  Two T-tables, A = Te0 and B = Te0 rotated right by
+// 8 bits, 32 copies each, in one 256-byte row per entry: A's copy c at byte
+// 256 e + 4 c, B's at 256 e + 128 + 4 c.  A ds_read_b32 serves its lanes in
+// two groups of 32 with banks (a/4) mod 32, so lane l reading copy l & 31 is
+// conflict-free whatever the state bytes, and the address is ONE v_perm of
+// the state word and the lane's offset (B: the instruction's offset 128).
+// With B, a column is A[a] ^ B[b] ^ ror16(A[c] ^ B[d] ^ ror16(rk)): one
+// rotate instead of three (rk16 holds the round keys rotated by 16).
+struct GcmLds {
+    uint32_t te[256 * 64];
+    struct PerWave {
+        uint32_t rk[60];
+        uint32_t rk16[60];
+        G128 th[16];
+        G128 t64[256];
+        uint4 stage[128];
+    } w[kGcmWaves];
+};
+#endif
 
 // Address of state byte k of word w in the 64-copy table.
 __device__ __forceinline__ uint32_t te_addr(uint32_t laneoff, uint32_t w, uint32_t k)
@@ -1150,11 +1180,14 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+#ifdef GCM_V1
 // N independent blocks at once (their table lookups interleave: more LDS
 // reads in flight per wave).
 template <int N>
-__device__ __forceinline__ void aes256_blocks_lds(const uint32_t *rk, const char *te, uint32_t laneoff, uint32_t (&st)[N][4])
+__device__ __forceinline__ void aes256_blocks_lds(const GcmLds::PerWave &PW, const char *te, uint32_t laneoff,
+                                                  uint32_t (&st)[N][4])
 {
+    const uint32_t *rk = PW.rk;
     auto T = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
     uint32_t s[N][4];
 #pragma unroll
@@ -1202,12 +1235,122 @@ __device__ __forceinline__ G128 gmul8(G128 x, const G128 *t, const uint64_t *rem
     }
     return z;
 }
+#else
+template <int N>
+__device__ __forceinline__ void aes256_blocks_lds(const GcmLds::PerWave &PW, const char *te, uint32_t laneoff,
+                                                  uint32_t (&st)[N][4])
+{
+    const uint32_t *rk = PW.rk, *rk16 = PW.rk16;
+    auto A = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
+    auto B = [&](uint32_t w, uint32_t k) {
+        return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k) + 128);
+    };
+    uint32_t s[N][4];
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+        for (int q = 0; q < 4; ++q) s[n][q] = st[n][q] ^ rk[q];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            uint32_t t[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t u = xor3(A(s[n][(q + 2) & 3], 1), B(s[n][(q + 3) & 3], 0), rk16[4 * r + q]);
+                t[q] = xor3(A(s[n][q], 3), B(s[n][(q + 1) & 3], 2), ror32(u, 16));
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s[n][q] = t[q];
+        }
+    }
+    // last round: S-box bytes (byte 2 of A's entries) gathered by v_perm
+    auto S4 = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        const uint32_t hi = __builtin_amdgcn_perm(A(a, 3), A(b, 2), 0x0602FFFFu);  // [Sa, Sb, -, -]
+        const uint32_t lo = __builtin_amdgcn_perm(A(c, 1), A(d, 0), 0xFFFF0602u);  // [-, -, Sc, Sd]
+        return (hi & 0xFFFF0000u) | (lo & 0xFFFFu);
+    };
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            st[n][q] = S4(s[n][q], s[n][(q + 1) & 3], s[n][(q + 2) & 3], s[n][(q + 3) & 3]) ^ rk[56 + q];
+}
+
+#ifndef GCM_STEP_REM
+// x * V with V's 8-bit table, reduced once.  x = sum over its bytes b_i
+// (i = 0: the top byte of hi, GCM's x^0..x^7) of b_i x^(8 i), so x V =
+// sum t[b_i] x^(8 i): each entry shifted right by 8 i bits into a 256-bit
+// sum D[0..7] (dwords, D[0] the most significant), then the part past x^127
+// folded back once, x^128 = 1 + x + x^2 + x^7.  The entries of one byte
+// offset (i = g, g + 4, g + 8, g + 12) add at whole dwords, so only four
+// partial sums are shifted; no reduction per byte (Horner's byte-by-byte
+// shift and reduce took twice the VALU), and no step waits on another.
+__device__ __forceinline__ G128 gmul8(G128 x, const G128 *t)
+{
+    const uint32_t xw[4] = {uint32_t(x.hi >> 32), uint32_t(x.hi), uint32_t(x.lo >> 32), uint32_t(x.lo)};
+    uint32_t D[8];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        uint32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const G128 e = t[(xw[j] >> (24 - 8 * g)) & 255u];
+            const uint32_t ew[4] = {uint32_t(e.hi >> 32), uint32_t(e.hi), uint32_t(e.lo >> 32), uint32_t(e.lo)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) a[j + k] ^= ew[k];
+        }
+        if (g == 0) {
+#pragma unroll
+            for (int k = 0; k < 7; ++k) D[k] = a[k];
+            D[7] = 0;
+        } else {
+            const uint32_t s = 8u * g;
+            D[0] ^= a[0] >> s;
+#pragma unroll
+            for (int k = 1; k < 7; ++k) D[k] ^= __builtin_amdgcn_alignbit(a[k - 1], a[k], s);
+            D[7] ^= a[6] << (32u - s);
+        }
+    }
+    // fold: V = D[4..7] (x^128..x^247, so V (1 + x + x^2 + x^7) stays below x^127)
+    uint32_t F[4];
+    F[0] = xor3(D[4], D[4] >> 1, D[4] >> 2) ^ (D[4] >> 7);
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+        F[k] = xor3(D[4 + k], __builtin_amdgcn_alignbit(D[3 + k], D[4 + k], 1),
+                    __builtin_amdgcn_alignbit(D[3 + k], D[4 + k], 2)) ^
+               __builtin_amdgcn_alignbit(D[3 + k], D[4 + k], 7);
+    return G128{uint64_t(D[0] ^ F[0]) << 32 | (D[1] ^ F[1]), uint64_t(D[2] ^ F[2]) << 32 | (D[3] ^ F[3])};
+}
+#else
+// x * V with V's 8-bit table (byte by byte from the last).  The 8 bits a
+// step shifts out, r, fold back as r * (1 + x^5 + x^6 + x^7) (GCM's
+// reflected 0xE1 || 0^120) into bits 49-63 of the high word: computed, not
+// looked up, so the serial chain through z holds no LDS read.
+__device__ __forceinline__ G128 gmul8(G128 x, const G128 *t)
+{
+    G128 z = t[uint32_t(x.lo) & 255u];
+#pragma unroll
+    for (int i = 14; i >= 0; --i) {
+        const uint32_t byte = i >= 8 ? uint32_t(x.lo >> (8 * (15 - i))) & 255u : uint32_t(x.hi >> (8 * (7 - i))) & 255u;
+        const G128 e = t[byte];
+        const uint32_t r = uint32_t(z.lo) & 255u;
+        const uint32_t u = xor3(r, r << 1, r << 2);  // r * (1 + x + x^2)
+        const uint32_t hh = xor3(uint32_t(z.hi >> 40), r << 17, u << 22);  // high dword of (z.hi >> 8) ^ rem
+        z.lo = (z.hi << 56) | (z.lo >> 8);
+        z.hi = ((uint64_t(hh) << 32) | uint32_t(z.hi >> 8)) ^ e.hi;
+        z.lo ^= e.lo;
+    }
+    return z;
+}
+#endif
+#endif
 
 __device__ __forceinline__ uint32_t be32(uint32_t x) { return __builtin_bswap32(x); }
 
 __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
 {
     __shared__ GcmLds L;
+#ifdef GCM_V1
     for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) L.te[i] = g_te0[i >> 6];
     for (uint32_t r = threadIdx.x; r < 256; r += blockDim.x) {
         uint64_t x = 0;
@@ -1216,6 +1359,11 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         L.rem8[r] = x << 48;
     }
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, laneoff = lane << 2;
+#else
+    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x)
+        L.te[i] = (i & 32u) ? ror32(g_te0[i >> 6], 8) : g_te0[i >> 6];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, laneoff = (lane & 31u) << 2;
+#endif
     const char *te = reinterpret_cast<const char *>(L.te);
     __syncthreads();
     // Persistent: one workgroup per CU; each wave takes pieces from a counter
@@ -1241,6 +1389,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         // this wave's tables (the previous piece's reads of them are done: the
         // wave barrier at the end of its loop body)
         for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk[i] = K.rk[i];
+#ifndef GCM_V1
+        for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk16[i] = ror32(K.rk[i], 16);
+#endif
         if (lane < 16) L.w[wv].th[lane] = K.th[lane];
         for (uint32_t i = lane; i < 256; i += 64) L.w[wv].t64[i] = K.t64[i];
         __builtin_amdgcn_s_waitcnt(0);
@@ -1263,9 +1414,18 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     j0[2] = (uint32_t(dn[8]) << 24 | uint32_t(dn[9]) << 16 | uint32_t(dn[10]) << 8 | dn[11]) ^ k;
     if (lane < 12) o[lane] = uint8_t(j0[lane >> 2] >> (24 - 8 * (lane & 3)));
     uint8_t *ct = o + 12;
-    const uint32_t *rk = L.w[wv].rk;
     const G128 *t64 = L.w[wv].t64;
     uint8_t *stage = reinterpret_cast<uint8_t *>(L.w[wv].stage);
+#ifndef GCM_LATE_LOADS
+    // The piece's plaintext as dwords from its aligned-down start (block i:
+    // dwords 4 i .. 4 i + 4, funnel-shifted by its offset in a dword).  A raw
+    // buffer returns 0 past its last dword, so every lane loads without a
+    // lane condition and a step's loads go out before its AES, which hides
+    // their latency (loads under a lane condition were waited for at once).
+    const uint32_t lastq = (pt_sh + m - 1) >> 2;
+    const __amdgpu_buffer_rsrc_t prs = gcm_rsrc(reinterpret_cast<uintptr_t>(pt) - pt_sh, uint64_t(lastq + 1) * 4);
+    const bool pt_fast = pt_sh == 0 && (m & 15u) == 0;  // whole aligned blocks: one 16-byte load each
+#endif
     // row j: blocks 64 j + lane (1 KiB of the piece), two rows per step (their
     // AES interleaved); lane: Horner in H^64 over its blocks, in order
     G128 Z = {0, 0};
@@ -1280,7 +1440,30 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             c[u][2] = j0[2];
             c[u][3] = 2 + 64 * (j + u) + lane;
         }
-        aes256_blocks_lds<2>(rk, te, laneoff, c);
+#ifndef GCM_LATE_LOADS
+        uint32_t px[2][5];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int32_t i = int32_t(64 * (j + u) + lane);
+            if (pt_fast) {
+                const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(prs, 16 * i, 0, 0));
+                px[u][0] = v.x;
+                px[u][1] = v.y;
+                px[u][2] = v.z;
+                px[u][3] = v.w;
+                px[u][4] = 0;
+            } else {
+                // dword by dword, clamped to the last one (a wide load that
+                // straddles the buffer's end may read as wholly out of range)
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    px[u][q] = __builtin_amdgcn_raw_buffer_load_b32(prs, int32_t(4 * min(uint32_t(4 * i + q), lastq)), 0, 0);
+            }
+        }
+#endif
+#ifndef GCM_DIAG_NO_AES
+        aes256_blocks_lds<2>(L.w[wv], te, laneoff, c);
+#endif
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const uint32_t i = 64 * (j + u) + lane;
@@ -1288,6 +1471,10 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             if (i < nb) {
                 const uint32_t bytes = min(16u, m - 16 * i);
                 uint32_t pw[4];
+#ifndef GCM_LATE_LOADS
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pw[q] = be32(__builtin_amdgcn_alignbit(px[u][q + 1], px[u][q], 8 * pt_sh));
+#else
                 if (pt_al && bytes == 16) {
                     const gu32 *q = reinterpret_cast<const gu32 *>(pt + 16 * i);
                     for (int k = 0; k < 4; ++k) pw[k] = be32(q[k]);
@@ -1304,6 +1491,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
                     for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
                     gcm_block_words(blk, pw);
                 }
+#endif
                 uint32_t w[4];
                 for (int q = 0; q < 4; ++q) w[q] = c[u][q] ^ pw[q];
                 if (bytes < 16) {  // the keystream past the piece's end is not ciphertext (nor hashed)
@@ -1313,19 +1501,45 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
                     }
                 }
                 cw = make_uint4(be32(w[0]), be32(w[1]), be32(w[2]), be32(w[3]));
+#if defined(GCM_DIAG_NO_GHASH)
+                Z = gx(Z, G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
+#elif defined(GCM_V1)
                 Z = gx(gmul8(Z, t64, L.rem8), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
+#else
+                Z = gx(gmul8(Z, t64), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
+#endif
                 ++cnt;
             }
             L.w[wv].stage[64 * u + lane] = cw;
         }
-        // the rows' ciphertext through LDS: 32 coalesced byte stores of 64 bytes
         __builtin_amdgcn_wave_barrier();
         const uint32_t row_bytes = min(2048u, m - 1024 * j);
+#ifdef GCM_BYTE_STORE
+        // the rows' ciphertext through LDS: 32 coalesced byte stores of 64 bytes
 #pragma unroll
         for (uint32_t q = 0; q < 32; ++q) {
             const uint32_t x = 64 * q + lane;
             if (x < row_bytes) ct[1024 * j + x] = stage[x];
         }
+#else
+        // the rows' ciphertext through LDS: the bytes up to the first aligned
+        // dword of the destination, then 8 coalesced dword stores (each dword
+        // funnel-shifted from two of the stage's), then the last 0-3 bytes
+        {
+            uint8_t *dst = ct + 1024 * j;
+            const uint32_t hb = min((4u - uint32_t(reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u, row_bytes);
+            const uint32_t nd = (row_bytes - hb) >> 2, tb = row_bytes - hb - 4 * nd;
+            const uint32_t *sw = reinterpret_cast<const uint32_t *>(stage);
+            uint32_t *dw = reinterpret_cast<uint32_t *>(dst + hb);
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                const uint32_t d = 64 * q + lane;
+                if (d < nd) dw[d] = __builtin_amdgcn_alignbit(sw[min(d + 1, 511u)], sw[d], 8 * hb);
+            }
+            if (lane < hb) dst[lane] = stage[lane];
+            if (lane < tb) dst[hb + 4 * nd + lane] = stage[hb + 4 * nd + lane];
+        }
+#endif
         __builtin_amdgcn_wave_barrier();
     }
     if (cnt) {
@@ -1339,7 +1553,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     if (lane == 0) {
         G128 S = gmul4(gx(Z, G128{0, uint64_t(m) * 8}), L.w[wv].th);
         uint32_t t[1][4] = {{j0[0], j0[1], j0[2], 1}};
-        aes256_blocks_lds<1>(rk, te, laneoff, t);
+        aes256_blocks_lds<1>(L.w[wv], te, laneoff, t);
         const uint64_t hi = S.hi ^ (uint64_t(t[0][0]) << 32 | t[0][1]), lo = S.lo ^ (uint64_t(t[0][2]) << 32 | t[0][3]);
         uint8_t *tag = ct + m;
         for (int q = 0; q < 8; ++q) {

@@ -179,6 +179,29 @@ def test_encode_device_resident_batch():
         encode.encode_device(t, offs, lens, small, key=KEY)
 
 
+def test_gcm_device_plaintext_at_every_alignment():
+    """GCM only (no LZ4): pieces read straight from the caller's buffer, at
+    every byte offset mod 16 and with ragged last blocks, whole pieces and
+    short ones, decrypt to their bytes."""
+    data = random_bytes(6 << 20, 91)
+    t = torch.from_numpy(data).cuda()
+    cuts, pos = [], 0
+    for i, n in enumerate([65536, 2 * 65536 + 5, 1000, 17, 3 * 65536 + 3, 65535, 16, 1, 4 * 65536, 70_001,
+                           31, 65536 + 16, 200_000, 48, 65537, 12345]):
+        pos += i % 16 + 1  # start at offset i mod 16 (+1) past the previous blob
+        cuts.append((pos, n))
+        pos += n
+    assert pos <= data.size
+    offs, lens = [c[0] for c in cuts], [c[1] for c in cuts]
+    cap = sum(encode.encode_bound(n, False, True) for n in lens)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    oo = encode.encode_device(t, offs, lens, out, key=KEY, compress=False)
+    host = out.cpu().numpy()
+    for i, (o, n) in enumerate(cuts):
+        enc = host[oo[i]:oo[i + 1]].tobytes()
+        assert ref.decode(enc, key=KEY, compressed=False) == data[o:o + n].tobytes(), (o, n)
+
+
 def test_backup_batch_device_encoder():
     """backup_batch with the device Encode: every blob in the packfiles opens
     under the repository key and inflates to its chunk (Decode, then the
