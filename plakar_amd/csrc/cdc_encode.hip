@@ -1276,6 +1276,91 @@ __device__ __forceinline__ void aes256_blocks_lds(const GcmLds::PerWave &PW, con
             st[n][q] = S4(s[n][q], s[n][(q + 1) & 3], s[n][(q + 2) & 3], s[n][(q + 3) & 3]) ^ rk[56 + q];
 }
 
+// Counter mode within one piece: the counter block is (J0[0..2], ctr) with
+// ctr < 2^16 (at most 4,097 blocks), so after the first AddRoundKey the
+// words s0..s2 and bytes 2-3 of s3 are the piece's constants.  Round 1's
+// outputs t2, t3 are then constants, and t0, t1 each depend on one counter
+// byte; round 2 takes 8 of its 16 lookups from t2, t3.  Those are done once
+// per piece (CtrPre, wave-uniform: SGPRs), leaving 2 + 8 lookups for rounds
+// 1-2 instead of 32 (counter-mode caching).
+struct CtrPre {
+    uint32_t p0t, p0u, p1t, p1u;  // round 1: t0 = p0t ^ ror16(p0u ^ B(s3, 0)), t1 = p1t ^ ror16(p1u ^ A(s3, 1))
+    uint32_t r0, w1, v1, w2, w3, v3;  // round 2's constant terms
+};
+
+__device__ __forceinline__ CtrPre ctr_pre(const GcmLds::PerWave &PW, const char *te, uint32_t laneoff,
+                                          const uint32_t (&j0)[3])
+{
+    const uint32_t *rk = PW.rk, *rk16 = PW.rk16;
+    auto A = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
+    auto B = [&](uint32_t w, uint32_t k) {
+        return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k) + 128);
+    };
+    auto u = [](uint32_t x) { return uint32_t(__builtin_amdgcn_readfirstlane(int(x))); };
+    const uint32_t s0 = j0[0] ^ rk[0], s1 = j0[1] ^ rk[1], s2 = j0[2] ^ rk[2], s3 = rk[3];  // s3: bytes 2-3 only
+    CtrPre c;
+    c.p0t = u(A(s0, 3) ^ B(s1, 2));
+    c.p0u = u(A(s2, 1) ^ rk16[4]);
+    c.p1t = u(A(s1, 3) ^ B(s2, 2));
+    c.p1u = u(B(s0, 0) ^ rk16[5]);
+    const uint32_t t2 = xor3(A(s2, 3), B(s3, 2), ror32(xor3(A(s0, 1), B(s1, 0), rk16[6]), 16));
+    const uint32_t t3 = xor3(A(s3, 3), B(s0, 2), ror32(xor3(A(s1, 1), B(s2, 0), rk16[7]), 16));
+    c.r0 = u(ror32(xor3(A(t2, 1), B(t3, 0), rk16[8]), 16));
+    c.w1 = u(B(t2, 2));
+    c.v1 = u(A(t3, 1) ^ rk16[9]);
+    c.w2 = u(A(t2, 3) ^ B(t3, 2));
+    c.w3 = u(A(t3, 3));
+    c.v3 = u(B(t2, 0) ^ rk16[11]);
+    return c;
+}
+
+// AES-256 of N counter blocks (J0[0..2], ctr[n]) of the piece CtrPre was made for.
+template <int N>
+__device__ __forceinline__ void aes256_ctr_lds(const GcmLds::PerWave &PW, const char *te, uint32_t laneoff,
+                                               const CtrPre &c, const uint32_t (&ctr)[N], uint32_t (&st)[N][4])
+{
+    const uint32_t *rk = PW.rk, *rk16 = PW.rk16;
+    auto A = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
+    auto B = [&](uint32_t w, uint32_t k) {
+        return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k) + 128);
+    };
+    uint32_t s[N][4];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        const uint32_t s3 = ctr[n] ^ rk[3];
+        const uint32_t t0 = c.p0t ^ ror32(c.p0u ^ B(s3, 0), 16);
+        const uint32_t t1 = c.p1t ^ ror32(c.p1u ^ A(s3, 1), 16);
+        s[n][0] = xor3(A(t0, 3), B(t1, 2), c.r0);
+        s[n][1] = xor3(A(t1, 3), c.w1, ror32(c.v1 ^ B(t0, 0), 16));
+        s[n][2] = c.w2 ^ ror32(xor3(A(t0, 1), B(t1, 0), rk16[10]), 16);
+        s[n][3] = xor3(c.w3, B(t0, 2), ror32(A(t1, 1) ^ c.v3, 16));
+    }
+#pragma unroll
+    for (int r = 3; r < 14; ++r) {
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+            uint32_t t[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t v = xor3(A(s[n][(q + 2) & 3], 1), B(s[n][(q + 3) & 3], 0), rk16[4 * r + q]);
+                t[q] = xor3(A(s[n][q], 3), B(s[n][(q + 1) & 3], 2), ror32(v, 16));
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s[n][q] = t[q];
+        }
+    }
+    auto S4 = [&](uint32_t a, uint32_t b, uint32_t cc, uint32_t d) {
+        const uint32_t hi = __builtin_amdgcn_perm(A(a, 3), A(b, 2), 0x0602FFFFu);
+        const uint32_t lo = __builtin_amdgcn_perm(A(cc, 1), A(d, 0), 0xFFFF0602u);
+        return (hi & 0xFFFF0000u) | (lo & 0xFFFFu);
+    };
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            st[n][q] = S4(s[n][q], s[n][(q + 1) & 3], s[n][(q + 2) & 3], s[n][(q + 3) & 3]) ^ rk[56 + q];
+}
+
 #ifndef GCM_STEP_REM
 // x * V with V's 8-bit table, reduced once.  x = sum over its bytes b_i
 // (i = 0: the top byte of hi, GCM's x^0..x^7) of b_i x^(8 i), so x V =
@@ -1414,6 +1499,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     j0[2] = (uint32_t(dn[8]) << 24 | uint32_t(dn[9]) << 16 | uint32_t(dn[10]) << 8 | dn[11]) ^ k;
     if (lane < 12) o[lane] = uint8_t(j0[lane >> 2] >> (24 - 8 * (lane & 3)));
     uint8_t *ct = o + 12;
+#if !defined(GCM_V1) && !defined(GCM_NO_CTR_PRE)
+    const CtrPre cpre = ctr_pre(L.w[wv], te, laneoff, j0);
+#endif
     const G128 *t64 = L.w[wv].t64;
     uint8_t *stage = reinterpret_cast<uint8_t *>(L.w[wv].stage);
 #ifndef GCM_LATE_LOADS
@@ -1461,8 +1549,14 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             }
         }
 #endif
-#ifndef GCM_DIAG_NO_AES
+#if defined(GCM_DIAG_NO_AES)
+#elif defined(GCM_V1) || defined(GCM_NO_CTR_PRE)
         aes256_blocks_lds<2>(L.w[wv], te, laneoff, c);
+#else
+        {
+            const uint32_t ctr[2] = {c[0][3], c[1][3]};
+            aes256_ctr_lds<2>(L.w[wv], te, laneoff, cpre, ctr, c);
+        }
 #endif
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
