@@ -1129,7 +1129,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t gcm_rsrc(uint64_t base, uint64
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, int(n), 0x00020000);
 }
 
+#if defined(GCM_ONE_ROW) && defined(GCM_ONE_ROW_12)
+constexpr uint32_t kGcmWaves = 12, kGcmRows = 1;
+#elif defined(GCM_ONE_ROW)
+constexpr uint32_t kGcmWaves = 16, kGcmRows = 1;  // one row per step, four waves per SIMD
+#else
 constexpr uint32_t kGcmWaves = 12;  // one workgroup per CU (LDS: the 64-KiB table), three waves per SIMD
+constexpr uint32_t kGcmRows = 2;    // rows of 64 blocks per step (their AES interleaved)
+#endif
 
 #ifdef GCM_V1
 // LDS of a GCM workgroup.  The T-table in 64 copies, entry e of copy c at
@@ -1145,7 +1152,7 @@ struct GcmLds {
         uint32_t rk[60];
         G128 th[16];
         G128 t64[256];
-        uint4 stage[128];
+        uint4 stage[64 * kGcmRows];
     } w[kGcmWaves];
 };
 #else
@@ -1164,7 +1171,7 @@ struct GcmLds {
         uint32_t rk16[60];
         G128 th[16];
         G128 t64[256];
-        uint4 stage[128];
+        uint4 stage[64 * kGcmRows];
     } w[kGcmWaves];
 };
 #endif
@@ -1519,19 +1526,19 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     G128 Z = {0, 0};
     uint32_t cnt = 0;
     const uint32_t rows = (nb + 63) / 64;
-    for (uint32_t j = 0; j < rows; j += 2) {
-        uint32_t c[2][4];
+    for (uint32_t j = 0; j < rows; j += kGcmRows) {
+        uint32_t c[kGcmRows][4];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < int(kGcmRows); ++u) {
             c[u][0] = j0[0];
             c[u][1] = j0[1];
             c[u][2] = j0[2];
             c[u][3] = 2 + 64 * (j + u) + lane;
         }
 #ifndef GCM_LATE_LOADS
-        uint32_t px[2][5];
+        uint32_t px[kGcmRows][5];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < int(kGcmRows); ++u) {
             const int32_t i = int32_t(64 * (j + u) + lane);
             if (pt_fast) {
                 const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(prs, 16 * i, 0, 0));
@@ -1551,15 +1558,17 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
 #endif
 #if defined(GCM_DIAG_NO_AES)
 #elif defined(GCM_V1) || defined(GCM_NO_CTR_PRE)
-        aes256_blocks_lds<2>(L.w[wv], te, laneoff, c);
+        aes256_blocks_lds<kGcmRows>(L.w[wv], te, laneoff, c);
 #else
         {
-            const uint32_t ctr[2] = {c[0][3], c[1][3]};
-            aes256_ctr_lds<2>(L.w[wv], te, laneoff, cpre, ctr, c);
+            uint32_t ctr[kGcmRows];
+#pragma unroll
+            for (uint32_t u = 0; u < kGcmRows; ++u) ctr[u] = c[u][3];
+            aes256_ctr_lds<kGcmRows>(L.w[wv], te, laneoff, cpre, ctr, c);
         }
 #endif
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < int(kGcmRows); ++u) {
             const uint32_t i = 64 * (j + u) + lane;
             uint4 cw = make_uint4(0, 0, 0, 0);
             if (i < nb) {
@@ -1607,11 +1616,11 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             L.w[wv].stage[64 * u + lane] = cw;
         }
         __builtin_amdgcn_wave_barrier();
-        const uint32_t row_bytes = min(2048u, m - 1024 * j);
+        const uint32_t row_bytes = min(1024u * kGcmRows, m - 1024 * j);
 #ifdef GCM_BYTE_STORE
         // the rows' ciphertext through LDS: 32 coalesced byte stores of 64 bytes
 #pragma unroll
-        for (uint32_t q = 0; q < 32; ++q) {
+        for (uint32_t q = 0; q < 16 * kGcmRows; ++q) {
             const uint32_t x = 64 * q + lane;
             if (x < row_bytes) ct[1024 * j + x] = stage[x];
         }
@@ -1626,9 +1635,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             const uint32_t *sw = reinterpret_cast<const uint32_t *>(stage);
             uint32_t *dw = reinterpret_cast<uint32_t *>(dst + hb);
 #pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) {
+            for (uint32_t q = 0; q < 4 * kGcmRows; ++q) {
                 const uint32_t d = 64 * q + lane;
-                if (d < nd) dw[d] = __builtin_amdgcn_alignbit(sw[min(d + 1, 511u)], sw[d], 8 * hb);
+                if (d < nd) dw[d] = __builtin_amdgcn_alignbit(sw[min(d + 1, 256u * kGcmRows - 1)], sw[d], 8 * hb);
             }
             if (lane < hb) dst[lane] = stage[lane];
             if (lane < tb) dst[hb + 4 * nd + lane] = stage[hb + 4 * nd + lane];
