@@ -703,7 +703,9 @@ def main():
                                                  dev=local)
 
                 def step():  # one whole backup of the share per step (an empty repository each time)
+                    t = time.perf_counter()
                     objs, _, st = session.run(paths, keep_packfiles=False)
+                    st["run_s"] = time.perf_counter() - t  # the Python call: wall_s + its Python side
                     backup_stats[0] = st
                     return objs
 

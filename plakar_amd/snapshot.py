@@ -46,6 +46,7 @@ device (batched) and the rest with hashlib on host threads, overlapped with
 the device work.
 """
 import concurrent.futures
+import gc
 import hashlib
 import warnings
 from dataclasses import dataclass, field
@@ -323,7 +324,16 @@ class BackupSession:
 
         fcb, pcb = _lib.BACKUP_FILE_FN(on_file), _lib.BACKUP_PACK_FN(on_pack)
         st = _lib.cdc_backup_stats()
-        _lib.check(_lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st)), "cdc_backup_files")
+        # The callbacks create an object per chunk; no cyclic collection
+        # (none of them forms a cycle) runs over the whole heap meanwhile.
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            rc = _lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st))
+        finally:
+            if gc_was:
+                gc.enable()
+        _lib.check(rc, "cdc_backup_files")
         if errors:
             raise errors[0]
         stats = {name: getattr(st, name) for name, _ in _lib.cdc_backup_stats._fields_}
