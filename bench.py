@@ -293,10 +293,11 @@ def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
     """Chunking + per-chunk SHA-256 and histograms (processChunk's device work,
     snapshot/backup.go:594-629) as a backup streams batches: passes chunk the
     rank's buffers on two alternating streams, and every `window` passes one
-    digest launch group on a third stream hashes the chunks of those passes
-    (a window's cut lists stay in HBM until their digests are done; two
-    windows alternate, so chunking runs ahead while the previous window
-    hashes).  Hashing a window at once is what fills the device: a SHA-256
+    digest launch group, on the next of four digest streams, hashes the
+    chunks of those passes (a window's cut lists stay in HBM until their
+    digests are done; two windows alternate, so chunking runs ahead while the
+    previous window hashes, and a window's longest chains overlap the next
+    window's launch).  Hashing a window at once is what fills the device: a SHA-256
     chain is serial per chunk, so a launch needs many chunks in flight (one
     C1 pass has ~11 K, the device keeps ~65 K lanes resident).  Combined GiB/s
     of input bytes; not part of `value`."""
@@ -322,8 +323,8 @@ def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
         cuts = [b.cuts[k] for b in sets[w] for k in range(b.n)]
         res = [b.res[k] for b in sets[w] for k in range(b.n)]
         hashed[w] = []
-        for g in range(0, len(wbufs), per):  # launch groups alternate over the digest streams
-            ds = dstreams[(g // per) % len(dstreams)]
+        for g in range(0, len(wbufs), per):  # launch groups (and rounds) alternate over the digest streams,
+            ds = dstreams[(r + g // per) % len(dstreams)]  # so one window's long chains overlap the next's
             for e in chunked[w]:
                 ds.wait_event(e)
             with torch.cuda.stream(ds):

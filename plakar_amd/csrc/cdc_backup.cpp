@@ -40,6 +40,7 @@
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -323,6 +324,28 @@ struct Run {
     std::unordered_set<Digest, DigestHash> seen;
     cdc_backup_stats st{};
     std::mutex stat_mu;
+    // CDC_BACKUP_TRACE=<path>: (seconds since the call began, event, batch,
+    // unit, bytes) per pipeline event, written there as CSV at the end; the
+    // device's stage events as offsets from trace_ref (recorded at the start)
+    Clock::time_point t0 = Clock::now();
+    const char *trace_path = std::getenv("CDC_BACKUP_TRACE");
+    struct Ev {
+        double t;
+        const char *what;
+        int64_t batch, unit;
+        uint64_t bytes;
+    };
+    std::vector<Ev> trace;
+    std::mutex trace_mu;
+    hipEvent_t trace_ref = nullptr;
+
+    void ev(const char *what, int64_t batch, int64_t unit = -1, uint64_t bytes = 0, double t = -1)
+    {
+        if (!trace_path) return;
+        if (t < 0) t = std::chrono::duration<double>(Clock::now() - t0).count();
+        std::lock_guard<std::mutex> lk(trace_mu);
+        trace.push_back(Ev{t, what, batch, unit, bytes});
+    }
 
     Run(cdc_backup *b, const char *const *p, int nn) : B(b), o(b->o), paths(p), n(nn) {}
 
@@ -470,9 +493,11 @@ void reader_main(Run &R)
             u.len = u.err == CDC_OK ? u.ne - u.start : 0;
         }
         uint8_t *dst = s.h_arena + u.arena_off;
+        R.ev("read", k, i, u.len);
         const auto t0 = Clock::now();
         int st = u.err == CDC_OK ? read_exact(R.paths[u.file], dst, u.start, u.len) : CDC_OK;
         const auto t1 = Clock::now();
+        R.ev("read_end", k, i, u.len);
         read_s += secs(t0, t1);
         bool wake;
         {
@@ -501,6 +526,7 @@ void reader_main(Run &R)
             }
         }
         hash_s += secs(t1, Clock::now());
+        R.ev("hash_end", k, i, u.len);
         {
             std::lock_guard<std::mutex> lk(R.mu);
             if (u.pieces > 1) F.hashed_pieces = u.piece + 1;
@@ -524,6 +550,7 @@ int sink(Run &R, cdc_packer *p)
     uint64_t len = 0;
     const int st = cdc::packer_seal(p, R.o.timestamp, &data, &len);
     if (st != CDC_OK) return st;
+    R.ev("packfile", -1, -1, len);
     std::lock_guard<std::mutex> lk(R.sink_mu);
     ++R.st.packfiles;
     R.st.packed_bytes += len;
@@ -613,6 +640,7 @@ int enqueue_cuts(Run &R, size_t k)
     const uint32_t nf = b.u1 - b.u0;
     hipStream_t st1 = R.B->stream[kA];
     const auto w0 = Clock::now();
+    R.ev("enq_cuts", int64_t(k), -1, b.bytes);
     HIPOK(hipEventRecord(s.ev[0], st1));
     HIPOK(hipMemcpyAsync(s.d_in, s.h_arena, b.bytes, hipMemcpyHostToDevice, st1));
     HIPOK(hipEventRecord(s.ev[1], st1));
@@ -663,6 +691,7 @@ int enqueue_digests(Run &R, size_t k)
     const uint32_t nf = b.u1 - b.u0;
     hipStream_t sd = R.B->stream[kD + int(k & 1)];
     const auto w0 = Clock::now();
+    R.ev("enq_digests", int64_t(k));
     HIPOK(hipStreamWaitEvent(sd, s.ev[2], 0));
     for (uint32_t j = 0; j < nf; ++j) {
         s.h_meta[3 * j] = s.cut0[j];
@@ -699,8 +728,18 @@ int finish_device(Run &R, size_t k)
     const Batch &b = R.batches[k];
     const uint32_t nf = b.u1 - b.u0;
     const auto w0 = Clock::now();
+    R.ev("finish_dev", int64_t(k));
     int st = wait_pumping(R, s.ev[5], k);
     if (st != CDC_OK) return st;
+    R.ev("lists_back", int64_t(k));
+    if (R.trace_path && R.trace_ref) {  // the device stages of batch k on the trace's clock
+        static const char *const kDevEv[6] = {"dev_h2d", "dev_h2d_end", "dev_cuts_end", "dev_dig", "dev_dig_end",
+                                              "dev_back_end"};
+        for (int e = 0; e < 6; ++e) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, R.trace_ref, s.ev[e]) == hipSuccess) R.ev(kDevEv[e], int64_t(k), -1, 0, ms * 1e-3);
+        }
+    }
     {  // a non-final piece: publish where the next piece starts (its reader waits for it)
         const Unit &u = R.units[b.u0];
         if (u.piece + 1 < u.pieces) {
@@ -820,6 +859,7 @@ int encode_job(Run &R, EncJob &J)
         if ((st = random_bytes(rnd.data(), rnd.size())) != CDC_OK) return st;
     }
     std::vector<uint64_t> oo(nb + 1, 0);
+    R.ev("encode", int64_t(J.k), -1, J.bound);
     const auto e0 = Clock::now();
     st = cdc_encode_device(R.B->device, s.d_in, J.off.data(), J.len.data(), nb, R.o.compress, R.o.key,
                            R.o.key ? rnd.data() : nullptr, s.d_enc, s.enc_cap, oo.data(), R.B->stream[kE]);
@@ -833,6 +873,7 @@ int encode_job(Run &R, EncJob &J)
     HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, R.B->stream[kE]));
     HIPOK(hipStreamSynchronize(R.B->stream[kE]));
     const auto e2 = Clock::now();
+    R.ev("encode_end", int64_t(J.k), -1, oo[nb]);
     {
         std::lock_guard<std::mutex> lk(R.mu);
         for (uint32_t q = 0; q < nb; ++q)
@@ -888,6 +929,7 @@ int finish_host(Run &R, size_t k)
     }
     if (R.status.load() != CDC_OK) return R.status.load();
     const auto cb0 = Clock::now();
+    R.ev("callbacks", int64_t(k));
     if (R.on_file) {
         static const cdc_cut kEmptyCut = {0, 0, 0};
         static const uint32_t kZeroHist[256] = {};
@@ -941,6 +983,7 @@ int finish_host(Run &R, size_t k)
         maybe_release(R, s);
     }
     R.cv.notify_all();
+    R.ev("callbacks_end", int64_t(k));
     std::lock_guard<std::mutex> lk(R.stat_mu);
     R.st.callback_s += secs(cb0, Clock::now());
     return CDC_OK;
@@ -1062,7 +1105,14 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
         uint64_t arena = 0, ncuts = 0, ws = 0, nfiles = 0;
         st = plan(R, arena, ncuts, ws, nfiles);
         R.st.slot_arena_bytes = arena;
+        R.ev("planned", -1, -1, uint64_t(R.batches.size()));
         if (st == CDC_OK && hipSetDevice(B->device) != hipSuccess) st = CDC_E_DEVICE;
+        if (st == CDC_OK && R.trace_path) {
+            if (hipEventCreate(&R.trace_ref) != hipSuccess || hipEventRecord(R.trace_ref, B->stream[kA]) != hipSuccess ||
+                hipEventSynchronize(R.trace_ref) != hipSuccess)
+                R.trace_ref = nullptr;
+            R.ev("trace_ref", -1);
+        }
         for (int i = 0; i < kSlots && st == CDC_OK && !R.batches.empty(); ++i) {
             st = grow_slot(B->slot[i], arena, ws, ncuts, nfiles);
             B->slot[i].batch = -1;
@@ -1153,6 +1203,17 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
         for (auto &sm : B->stream) (void)hipStreamSynchronize(sm);
     }
     R.st.wall_s = secs(w0, Clock::now());
+    R.ev("end", -1);
+    if (R.trace_path) {
+        if (FILE *f = std::fopen(R.trace_path, "w")) {
+            std::fprintf(f, "t_s,event,batch,unit,bytes\n");
+            for (const auto &e : R.trace)
+                std::fprintf(f, "%.6f,%s,%lld,%lld,%llu\n", e.t, e.what, (long long)e.batch, (long long)e.unit,
+                             (unsigned long long)e.bytes);
+            std::fclose(f);
+        }
+        if (R.trace_ref) (void)hipEventDestroy(R.trace_ref);
+    }
     R.st.hw_queues = B->hw_queues;
     R.st.streams_serialised = B->hw_queues < 8 ? 1 : 0;
     if (stats) *stats = R.st;

@@ -1496,7 +1496,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint32_t m = uint32_t(min<uint64_t>(kPiece, F - p0));  // piece bytes
     const uint32_t nb = (m + 15) / 16;
     const gu8 *pt = reinterpret_cast<const gu8 *>(reinterpret_cast<uintptr_t>(plain_ptr(B, b) + p0));
+#ifdef GCM_LATE_LOADS
     const bool pt_al = (reinterpret_cast<uintptr_t>(pt) & 15u) == 0;
+#endif
     const uint32_t pt_sh = uint32_t(reinterpret_cast<uintptr_t>(pt) & 3u);
     uint8_t *o = B.out + B.out_off[b] + 60 + uint64_t(k) * (kPiece + 28);
     const uint8_t *dn = B.rnd + 56ull * b + 44;  // data nonce
