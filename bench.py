@@ -295,9 +295,9 @@ def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
     rank's buffers on two alternating streams, and every `window` passes one
     digest launch group, on the next of four digest streams, hashes the
     chunks of those passes (a window's cut lists stay in HBM until their
-    digests are done; two windows alternate, so chunking runs ahead while the
-    previous window hashes, and a window's longest chains overlap the next
-    window's launch).  Hashing a window at once is what fills the device: a SHA-256
+    digests are done; three windows rotate, so chunking runs ahead while the
+    previous windows hash, and a window's longest chains overlap the next
+    windows' launches).  Hashing a window at once is what fills the device: a SHA-256
     chain is serial per chunk, so a launch needs many chunks in flight (one
     C1 pass has ~11 K, the device keeps ~65 K lanes resident).  Combined GiB/s
     of input bytes; not part of `value`."""
@@ -305,14 +305,16 @@ def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
     from plakar_amd import hashing
     cstreams = [torch.cuda.Stream(dev) for _ in range(2)]
     dstreams = [torch.cuda.Stream(dev) for _ in range(4)]
-    sets = [[devmod.DeviceBatch(bufs, opts, final=True, device=dev.index) for _ in range(window)] for _ in range(2)]
-    chunked = [[torch.cuda.Event() for _ in range(window)] for _ in range(2)]
-    hashed = [[], []]
+    nsets = 3  # windows in flight: a window's longest chains overlap the next two windows' launches
+    sets = [[devmod.DeviceBatch(bufs, opts, final=True, device=dev.index) for _ in range(window)]
+            for _ in range(nsets)]
+    chunked = [[torch.cuda.Event() for _ in range(window)] for _ in range(nsets)]
+    hashed = [[] for _ in range(nsets)]
     wbufs = [t for _ in range(window) for t in bufs]
     per = len(wbufs)  # one launch group per window (descriptors in device memory past 32 buffers)
 
     def one_round(r):
-        w = r % 2
+        w = r % nsets
         for i in range(window):
             s = cstreams[i % 2]
             if i < 2:  # the set's previous digests are done with its cut lists
@@ -332,7 +334,7 @@ def chunk_digest_pipeline(torch, bufs, opts, dev, window, rounds):
             ev = torch.cuda.Event()
             ev.record(ds)
             hashed[w].append(ev)
-    for r in range(2):  # warm-up
+    for r in range(nsets):  # warm-up
         one_round(r)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()

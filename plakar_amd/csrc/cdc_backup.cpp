@@ -310,7 +310,9 @@ struct Run {
     std::vector<Unit> units;
     std::vector<Batch> batches;
     std::vector<uint32_t> batch_of;  // per unit
-    std::atomic<uint32_t> next_unit{0};
+    uint32_t next_read = 0;        // the next unit to read (guarded by mu)
+    uint32_t reading = 0;          // reads in progress (guarded by mu)
+    std::deque<uint32_t> hash_q;   // units read, not yet hashed, oldest first (guarded by mu)
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
@@ -454,73 +456,112 @@ void maybe_release(Run &R, Slot &s)
     }
 }
 
-// Reader threads: unit after unit in batch order (a slot is claimed by the
-// first unit of its batch once the batch kSlots back released it), each unit
-// read into the slot's arena and then hashed there (the object checksum, one
-// serial chain: a large file's hash no longer holds back the batch's reads or
-// the next batch; it gates only the callbacks and the slot's release).  Piece
-// j > 0 of a large file waits for piece j - 1's carried next start (its cut
-// list back from the device) before it reads, and for piece j - 1's hash
-// before it continues the object hash.  A file that cannot be read is marked
-// failed and the run goes on.
+// Reader threads.  Two kinds of task: reading unit after unit, in batch
+// order, into its batch's slot (a slot is claimed by the first unit of its
+// batch once the batch kSlots back released it), and hashing a unit that is
+// read (the object checksum, one serial chain per file: a 124-MiB file is
+// ~62 ms on a host core).  A thread takes the next read whenever it can
+// start, else the oldest hash it can start, so the device's input is never
+// queued behind object hashes (when each reader hashed what it had just
+// read, the 16 largest files held all 16 readers for up to 60 ms while the
+// device waited for the next batch: profiles/r04_c4b_trace.txt).  Piece
+// j > 0 of a large file is read once piece j - 1's carried next start is
+// back from the device, and hashed once piece j - 1 is hashed.  A file that
+// cannot be read is marked failed and the run goes on.
+bool read_ready_locked(Run &R)  // the next unit's read can start (R.mu held)
+{
+    if (R.next_read >= R.units.size()) return false;
+    const uint32_t i = R.next_read, k = R.batch_of[i];
+    const Slot &s = R.B->slot[k % kSlots];
+    if (!(s.batch == int(k) || (s.batch < 0 && s.next == int(k)))) return false;
+    const Unit &u = R.units[i];
+    const FileState &F = R.files[u.file];
+    return u.piece == 0 || F.err != CDC_OK || F.dev_pieces >= u.piece;
+}
+
+bool hash_ready_locked(Run &R, uint32_t i)  // unit i's bytes can go into its object hash (R.mu held)
+{
+    const Unit &u = R.units[i];
+    return u.pieces == 1 || R.files[u.file].hashed_pieces >= u.piece;
+}
+
 void reader_main(Run &R)
 {
     double read_s = 0, hash_s = 0;
-    for (uint32_t i; (i = R.next_unit.fetch_add(1)) < uint32_t(R.units.size()) && R.status.load() == CDC_OK;) {
+    for (;;) {
+        uint32_t i = 0;
+        bool is_read = false;
+        {
+            std::unique_lock<std::mutex> lk(R.mu);
+            size_t h = 0;
+            R.cv.wait(lk, [&] {
+                if (R.status.load() != CDC_OK) return true;
+                if ((is_read = read_ready_locked(R))) return true;
+                for (h = 0; h < R.hash_q.size(); ++h)
+                    if (hash_ready_locked(R, R.hash_q[h])) return true;
+                return R.next_read >= R.units.size() && R.reading == 0 && R.hash_q.empty();
+            });
+            if (R.status.load() != CDC_OK) break;
+            if (is_read) {
+                i = R.next_read++;
+                ++R.reading;
+                const uint32_t k = R.batch_of[i];
+                Slot &s = R.B->slot[k % kSlots];
+                if (s.batch != int(k)) {
+                    s.batch = int(k);
+                    s.next = int(k) + kSlots;
+                    s.read_done = s.hash_done = s.device_done = false;
+                    s.nread = s.nhashed = 0;
+                    s.pending = 0;
+                }
+                Unit &u = R.units[i];
+                FileState &F = R.files[u.file];
+                u.err = F.err;
+                u.start = u.piece ? F.next_start : 0;
+                u.len = u.err == CDC_OK ? u.ne - u.start : 0;
+            } else if (h < R.hash_q.size()) {
+                i = R.hash_q[h];
+                R.hash_q.erase(R.hash_q.begin() + std::ptrdiff_t(h));
+            } else {
+                break;  // every unit read and hashed
+            }
+        }
         const uint32_t k = R.batch_of[i];
         const Batch &b = R.batches[k];
         Slot &s = R.B->slot[k % kSlots];
         Unit &u = R.units[i];
         FileState &F = R.files[u.file];
-        {
-            std::unique_lock<std::mutex> lk(R.mu);
-            R.cv.wait(lk, [&] {
-                return R.status.load() != CDC_OK || s.batch == int(k) || (s.batch < 0 && s.next == int(k));
-            });
-            if (R.status.load() != CDC_OK) break;
-            if (s.batch != int(k)) {
-                s.batch = int(k);
-                s.next = int(k) + kSlots;
-                s.read_done = s.hash_done = s.device_done = false;
-                s.nread = s.nhashed = 0;
-                s.pending = 0;
-            }
-            if (u.piece)  // the previous piece's cut list is back (or the file failed)
-                R.cv.wait(lk, [&] { return R.status.load() != CDC_OK || F.err != CDC_OK || F.dev_pieces >= u.piece; });
-            if (R.status.load() != CDC_OK) break;
-            u.err = F.err;
-            u.start = u.piece ? F.next_start : 0;
-            u.len = u.err == CDC_OK ? u.ne - u.start : 0;
-        }
         uint8_t *dst = s.h_arena + u.arena_off;
-        R.ev("read", k, i, u.len);
-        const auto t0 = Clock::now();
-        int st = u.err == CDC_OK ? read_exact(R.paths[u.file], dst, u.start, u.len) : CDC_OK;
-        const auto t1 = Clock::now();
-        R.ev("read_end", k, i, u.len);
-        read_s += secs(t0, t1);
-        bool wake;
-        {
-            std::lock_guard<std::mutex> lk(R.mu);
-            if (st != CDC_OK) {
-                u.err = st;
-                u.len = 0;
-                if (F.err == CDC_OK) F.err = st;
+        if (is_read) {
+            R.ev("read", k, i, u.len);
+            const auto t0 = Clock::now();
+            const int st = u.err == CDC_OK ? read_exact(R.paths[u.file], dst, u.start, u.len) : CDC_OK;
+            read_s += secs(t0, Clock::now());
+            R.ev("read_end", k, i, u.len);
+            {
+                std::lock_guard<std::mutex> lk(R.mu);
+                if (st != CDC_OK) {
+                    u.err = st;
+                    u.len = 0;
+                    if (F.err == CDC_OK) F.err = st;
+                }
+                if (++s.nread == b.u1 - b.u0) s.read_done = true;
+                --R.reading;
+                R.hash_q.push_back(i);
             }
-            wake = ++s.nread == b.u1 - b.u0;
-            s.read_done = s.read_done || wake;
+            R.cv.notify_all();
+            continue;
         }
-        R.cv.notify_all();
-        if (u.err == CDC_OK && u.pieces == 1) {
-            cdc::sha256(dst, u.len, F.obj);
-        } else if (u.pieces > 1) {
+        const auto t1 = Clock::now();
+        {
             bool go;
             {
-                std::unique_lock<std::mutex> lk(R.mu);
-                R.cv.wait(lk, [&] { return R.status.load() != CDC_OK || F.hashed_pieces >= u.piece; });
-                go = F.err == CDC_OK && u.err == CDC_OK && R.status.load() == CDC_OK;
+                std::lock_guard<std::mutex> lk(R.mu);
+                go = u.err == CDC_OK && (u.pieces == 1 || F.err == CDC_OK);
             }
-            if (go) {  // the bytes this piece adds: [nb, ne) of the file
+            if (go && u.pieces == 1) {
+                cdc::sha256(dst, u.len, F.obj);
+            } else if (go) {  // the bytes this piece adds: [nb, ne) of the file
                 F.sha.update(dst + (u.nb - u.start), size_t(u.ne - u.nb));
                 if (u.piece + 1 == u.pieces) F.sha.final(F.obj);
             }
@@ -530,8 +571,7 @@ void reader_main(Run &R)
         {
             std::lock_guard<std::mutex> lk(R.mu);
             if (u.pieces > 1) F.hashed_pieces = u.piece + 1;
-            wake = ++s.nhashed == b.u1 - b.u0;
-            if (wake) {
+            if (++s.nhashed == b.u1 - b.u0) {
                 s.hash_done = true;
                 maybe_release(R, s);
             }

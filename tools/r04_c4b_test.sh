@@ -1,0 +1,8 @@
+#!/bin/bash
+# The backup tests, then c4b with its pipeline trace.
+O=gpurun_out/${1:-r04c4bx}; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest tests/test_backup.py tests/test_backup_cpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_backup.log 2>&1 || { tail -30 $O/pytest_backup.log; exit 1; }
+tail -1 $O/pytest_backup.log
+bash tools/r04_c4b_trace.sh ${1:-r04c4bx}/c4b
