@@ -171,7 +171,15 @@ struct Slot {
 #define CDC_BACKUP_SLOTS 6
 #endif
 constexpr int kSlots = CDC_BACKUP_SLOTS;
-constexpr int kA = 0, kD = 1, kE = 3;  // cdc_backup::stream; digests alternate over kD, kD + 1
+// cdc_backup::stream: scans kA, H2D kH, digests alternate over kD, kD + 1,
+// the two encoder threads kE and kE + 2
+constexpr int kA = 0, kD = 1, kE = 3, kH = 4;
+constexpr int kEncoders = 2;  // one's kernels run beside the other's copy-back (~10 ms per 512-MiB batch)
+// The pipeline's scans run persistent (tasks from a counter, ~2 per wave): a
+// static grid needs every CU, and the CUs held by the other streams' digest
+// launches (66 KiB of LDS per workgroup, ~10-18 ms each) left the scan's last
+// workgroups waiting 4-5 ms per batch (profiles/r04_c4b_devtrace.txt).
+constexpr int kBackupScanTpw = 2;
 
 #define HIPOK(x)                                         \
     do {                                                 \
@@ -276,7 +284,7 @@ struct cdc_backup {
     // Encode's own: independent only with GPU_MAX_HW_QUEUES >= 8 (HIP's
     // default of 4 maps several streams onto one hardware queue, which
     // serialises them).
-    hipStream_t stream[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t stream[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     int hw_queues = 0;  // GPU_MAX_HW_QUEUES at cdc_backup_new (0: unset)
 };
 
@@ -290,7 +298,7 @@ struct Blob {
 };
 
 // Encode of one batch's new chunks, handed from the calling thread to the
-// encoder thread once the batch is deduplicated.
+// encoder threads once the batch is deduplicated.
 struct EncJob {
     size_t k;
     std::vector<uint64_t> off, len;
@@ -312,7 +320,7 @@ struct Run {
     std::vector<uint32_t> batch_of;  // per unit
     uint32_t next_read = 0;        // the next unit to read (guarded by mu)
     uint32_t reading = 0;          // reads in progress (guarded by mu)
-    std::deque<uint32_t> hash_q;   // units read, not yet hashed, oldest first (guarded by mu)
+    std::deque<uint32_t> hash_q;   // units read, not yet hashed, in unit order (guarded by mu)
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
@@ -461,10 +469,11 @@ void maybe_release(Run &R, Slot &s)
 // batch once the batch kSlots back released it), and hashing a unit that is
 // read (the object checksum, one serial chain per file: a 124-MiB file is
 // ~62 ms on a host core).  A thread takes the next read whenever it can
-// start, else the oldest hash it can start, so the device's input is never
-// queued behind object hashes (when each reader hashed what it had just
-// read, the 16 largest files held all 16 readers for up to 60 ms while the
-// device waited for the next batch: profiles/r04_c4b_trace.txt).  Piece
+// start, else the first hash in unit order that it can start, so the
+// device's input is never queued behind object hashes (when each reader
+// hashed what it had just read, the 16 largest files held all 16 readers for
+// up to 60 ms while the device waited for the next batch:
+// profiles/r04_c4b_trace.txt).  Piece
 // j > 0 of a large file is read once piece j - 1's carried next start is
 // back from the device, and hashed once piece j - 1 is hashed.  A file that
 // cannot be read is marked failed and the run goes on.
@@ -547,7 +556,9 @@ void reader_main(Run &R)
                 }
                 if (++s.nread == b.u1 - b.u0) s.read_done = true;
                 --R.reading;
-                R.hash_q.push_back(i);
+                // hashes go in unit order (batch order, largest file first),
+                // not in the order reads end: a large file's read ends late
+                R.hash_q.insert(std::upper_bound(R.hash_q.begin(), R.hash_q.end(), i), i);
             }
             R.cv.notify_all();
             continue;
@@ -678,12 +689,15 @@ int enqueue_cuts(Run &R, size_t k)
     const Batch &b = R.batches[k];
     const cdc_opts *co = &R.o.chunking;
     const uint32_t nf = b.u1 - b.u0;
-    hipStream_t st1 = R.B->stream[kA];
+    hipStream_t st1 = R.B->stream[kA], sh = R.B->stream[kH];
     const auto w0 = Clock::now();
     R.ev("enq_cuts", int64_t(k), -1, b.bytes);
-    HIPOK(hipEventRecord(s.ev[0], st1));
-    HIPOK(hipMemcpyAsync(s.d_in, s.h_arena, b.bytes, hipMemcpyHostToDevice, st1));
-    HIPOK(hipEventRecord(s.ev[1], st1));
+    // H2D on its own stream: batch k + 1's copy does not wait behind batch
+    // k's scan (which waits for CUs beside the digest launches)
+    HIPOK(hipEventRecord(s.ev[0], sh));
+    HIPOK(hipMemcpyAsync(s.d_in, s.h_arena, b.bytes, hipMemcpyHostToDevice, sh));
+    HIPOK(hipEventRecord(s.ev[1], sh));
+    HIPOK(hipStreamWaitEvent(st1, s.ev[1], 0));
     std::vector<const void *> dp(nf);
     std::vector<uint64_t> caps(nf);
     std::vector<cdc_cut *> cp(nf);
@@ -852,7 +866,7 @@ int finish_device(Run &R, size_t k)
     const uint32_t nb = uint32_t(enc_off.size());
     const bool encode = nb && (R.o.compress || R.o.key);
     {
-        // The new chunks go to the encoder thread (Encode, then the encoded
+        // The new chunks go to the encoder threads (Encode, then the encoded
         // blobs back, then the packers), so this thread goes on driving the
         // next batches instead of waiting out Encode; the slot stays held
         // until its blobs are packed.
@@ -884,10 +898,14 @@ int finish_device(Run &R, size_t k)
     return CDC_OK;
 }
 
-// The encoder thread: each batch's new chunks through Encode (LZ4 frame +
-// AES-256-GCM on the device, stream E), the encoded blobs back to pinned
-// memory, then to the packers; batches in order.
-int encode_job(Run &R, EncJob &J)
+// The encoder threads (two, each with its own stream and Encode workspace,
+// taking batches in turn): a batch's new chunks through Encode (LZ4 frame +
+// AES-256-GCM on the device), the encoded blobs back to pinned memory, then
+// to the packers.  The copy back of one batch (~10 ms for 512 MiB over PCIe)
+// overlaps the next batch's Encode kernels; with one thread the batches'
+// Encodes ran end to end and set the end of the run
+// (profiles/r04_c4b_trace.txt).
+int encode_job(Run &R, EncJob &J, hipStream_t se)
 {
     Slot &s = R.B->slot[J.k % kSlots];
     const uint32_t nb = uint32_t(J.off.size());
@@ -902,7 +920,7 @@ int encode_job(Run &R, EncJob &J)
     R.ev("encode", int64_t(J.k), -1, J.bound);
     const auto e0 = Clock::now();
     st = cdc_encode_device(R.B->device, s.d_in, J.off.data(), J.len.data(), nb, R.o.compress, R.o.key,
-                           R.o.key ? rnd.data() : nullptr, s.d_enc, s.enc_cap, oo.data(), R.B->stream[kE]);
+                           R.o.key ? rnd.data() : nullptr, s.d_enc, s.enc_cap, oo.data(), se);
     if (st != CDC_OK) return st;
     const auto e1 = Clock::now();
     if (oo[nb] > s.henc_cap || !s.h_enc) {
@@ -910,8 +928,8 @@ int encode_job(Run &R, EncJob &J)
         if ((st = grow_host(s.h_enc, want, 0)) != CDC_OK) return st;
         s.henc_cap = want;
     }
-    HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, R.B->stream[kE]));
-    HIPOK(hipStreamSynchronize(R.B->stream[kE]));
+    HIPOK(hipMemcpyAsync(s.h_enc, s.d_enc, oo[nb], hipMemcpyDeviceToHost, se));
+    HIPOK(hipStreamSynchronize(se));
     const auto e2 = Clock::now();
     R.ev("encode_end", int64_t(J.k), -1, oo[nb]);
     {
@@ -927,12 +945,14 @@ int encode_job(Run &R, EncJob &J)
     return CDC_OK;
 }
 
-void encoder_main(Run &R)
+void encoder_main(Run &R, int idx)
 {
     if (hipSetDevice(R.B->device) != hipSuccess) {
         R.fail(CDC_E_DEVICE);
         return;
     }
+    cdc::t_encode_ws = idx;
+    hipStream_t se = R.B->stream[idx ? kE + 2 : kE];
     for (;;) {
         EncJob J;
         {
@@ -944,7 +964,7 @@ void encoder_main(Run &R)
         }
         int st;
         try {
-            st = encode_job(R, J);
+            st = encode_job(R, J, se);
         } catch (const std::bad_alloc &) {
             st = CDC_E_NOMEM;
         }
@@ -1132,6 +1152,11 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
 {
     if (!B || n < 0 || (n && !paths)) return CDC_E_INVALID;
     const auto w0 = Clock::now();
+    struct ScanMode {  // this thread's scans (workspace sizing and launches) persistent for the call
+        int prev = cdc::t_scan_tpw;
+        ScanMode() { cdc::t_scan_tpw = kBackupScanTpw; }
+        ~ScanMode() { cdc::t_scan_tpw = prev; }
+    } scan_mode;
     Run *Rp = new (std::nothrow) Run(B, paths, n);
     if (!Rp) return CDC_E_NOMEM;
     Run &R = *Rp;
@@ -1140,7 +1165,8 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
     R.ctx = ctx;
     int st = CDC_OK;
     std::vector<std::thread> readers, packers;
-    std::thread callbacks, encoder;
+    std::thread callbacks;
+    std::vector<std::thread> encoders;
     try {
         uint64_t arena = 0, ncuts = 0, ws = 0, nfiles = 0;
         st = plan(R, arena, ncuts, ws, nfiles);
@@ -1175,7 +1201,7 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
             const int nr = std::max(1, R.o.readers ? R.o.readers : 8);
             for (int r = 0; r < nr; ++r) readers.emplace_back([&R] { reader_main(R); });
             callbacks = std::thread([&R] { callback_main(R); });
-            encoder = std::thread([&R] { encoder_main(R); });
+            for (int e = 0; e < kEncoders; ++e) encoders.emplace_back([&R, e] { encoder_main(R, e); });
             for (int p = 0; p < np; ++p) {
                 cdc_packer *pk = B->packers[size_t(p)];
                 packers.emplace_back([&R, pk] { packer_main(R, pk); });
@@ -1208,7 +1234,8 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
                 R.stop_encoder = true;
             }
             R.cv.notify_all();
-            if (encoder.joinable()) encoder.join();
+            for (auto &t : encoders) t.join();
+            encoders.clear();
             if (st == CDC_OK && callbacks.joinable()) {
                 callbacks.join();  // the last slots are released by the callbacks
                 st = R.status.load();
@@ -1227,13 +1254,13 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
         st = CDC_E_DEVICE;
         R.fail(st);
     }
-    if (encoder.joinable()) {
+    if (!encoders.empty()) {
         {
             std::lock_guard<std::mutex> lk(R.mu);
             R.stop_encoder = true;
         }
         R.cv.notify_all();
-        encoder.join();
+        for (auto &t : encoders) t.join();
     }
     if (callbacks.joinable()) callbacks.join();
     for (auto &t : readers) t.join();

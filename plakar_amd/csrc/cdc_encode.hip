@@ -1726,9 +1726,16 @@ struct WsCache {
     hipStream_t aux = nullptr;  // k_xxh32 runs here, beside the LZ4 and GCM kernels
     hipEvent_t fork = nullptr, join = nullptr;
 };
-static WsCache g_ws[64];
+// Two per device: a caller that runs two Encode calls at once (the backup
+// pipeline's two encoder threads) picks the second with cdc::t_encode_ws = 1,
+// so one call's kernels run beside the other's copy-back.
+static WsCache g_ws[64][2];
 
 }  // namespace enc
+
+namespace cdc {
+thread_local int t_encode_ws = 0;
+}
 
 using namespace enc;
 
@@ -1795,7 +1802,7 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     const size_t o_oo = take((nb + 1) * 8), o_pb = take((nb + 1) * 4), o_keys = take(encrypt ? nb * sizeof(BlobKey) : 0);
     const size_t o_status = take(16), o_frames = take(encrypt ? slot : 0), o_xx = take(compress ? nb * 4 : 0);
     if (device < 0 || device >= 64) return CDC_E_INVALID;
-    WsCache &C = g_ws[device];
+    WsCache &C = g_ws[device][cdc::t_encode_ws & 1];
     std::lock_guard<std::mutex> lk(C.mu);
     if (C.cap < off) {
         if (C.p) (void)hipFree(C.p);

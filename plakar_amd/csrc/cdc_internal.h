@@ -132,6 +132,12 @@ int launch_entropy(const uint32_t *d_hist, uint64_t rows, double *d_out, void *s
 int launch_arena_cuts(const uint64_t *d_meta, uint32_t nfiles, const cdc_result *d_res, const cdc_cut *d_cuts,
                       cdc_cut *d_out, void *stream);
 extern uint64_t g_digest_lanes;
+// The calling thread's scan mode for make_plan: -1 the default (static grid,
+// or CDC_SCAN_TASKS_PER_WAVE), k >= 0 the persistent scan with about k tasks
+// per wave (0: the static grid).
+extern thread_local int t_scan_tpw;
+// The calling thread's Encode workspace (0 or 1) for cdc_encode_device.
+extern thread_local int t_encode_ws;
 
 // cdc_api.cpp: a host-buffer pipeline on one device that outlives one call
 // (the collector's per-device worker).  The source hands out batches of at

@@ -494,19 +494,21 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     const char *tab = s_lds;
     if (!act) return;
     // Persistent mode (B.persist, k_scan / k_scan_f): one workgroup per CU;
-    // a wave's first task is static (blockIdx.x * kS2Waves + wave), later
-    // ones come from a per-launch atomic counter (W.tick[2], zeroed by the
-    // host before the launch), so CUs that run ahead (the end times spread by
-    // XCD, most at a cold clock) take more of the buffer.
+    // every task comes from a per-launch atomic counter (W.tick[2], zeroed by
+    // the host before the launch), so the CUs that run ahead take more of the
+    // buffer, and a workgroup that starts late (its CU held by another
+    // stream's kernel) finds the tasks taken instead of holding the launch.
     const bool persist = !kMaskL && B.persist != 0;
-    const uint32_t nwaves = gridDim.x * kS2Waves;
-    for (uint32_t cur = task;;) {
+    auto next_task = [&]() {
+        uint32_t t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(W.tick + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return uint32_t(__builtin_amdgcn_readfirstlane(t));
+    };
+    for (uint32_t cur = persist ? next_task() : task;;) {
         if (cur >= B.total_tasks) break;
         scan_task<kMaskL, kFused>(B, P, W, s_lds, tab, cur, lane, wave, laneoff);
         if (!persist) break;
-        uint32_t t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(W.tick + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cur = nwaves + uint32_t(__builtin_amdgcn_readfirstlane(t));
+        cur = next_task();
     }
     if (clk && threadIdx.x == 0) {
         g_ts[clk + 2] = __builtin_amdgcn_s_memrealtime();
@@ -2424,11 +2426,14 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     // static grid at every k (2: -3 %, 3: -4 %, 6: -12 % on the driver's
     // command; shorter lanes add lead bytes and a pipeline fill per task), so
     // the default is the static grid (0).
-    static const uint64_t persist_tpw = [] {
+    static const uint64_t env_tpw = [] {
         const char *e = getenv("CDC_SCAN_TASKS_PER_WAVE");
         const long v = e ? atol(e) : 0;
         return uint64_t(v >= 0 && v <= 64 ? v : 0);
     }();
+    // the calling thread's override (the backup pipeline's scans share the
+    // device with digest launches, cdc_backup.cpp)
+    const uint64_t persist_tpw = t_scan_tpw >= 0 && t_scan_tpw <= 64 ? uint64_t(t_scan_tpw) : env_tpw;
     uint64_t wgs = persist_tpw ? cus : (cus > 16 ? cus - 7 : cus);
     if (const char *env = getenv("CDC_SCAN_WGS")) {
         const long v = atol(env);
