@@ -45,6 +45,7 @@ file.  object_hash="auto" hashes files up to `device_object_max` bytes on the
 device (batched) and the rest with hashlib on host threads, overlapped with
 the device work.
 """
+import collections.abc
 import concurrent.futures
 import gc
 import hashlib
@@ -59,6 +60,51 @@ from . import chunkers, device, hashing
 from .repository import Repository
 
 # ------------------------------------------------------------------- records
+class ChunkRecords(collections.abc.Sequence):
+    """The chunks of one object as the native backup pipeline reports them
+    (objects.Chunk's fields, objects/objects.go:73-79): digests, lengths,
+    entropies and byte histograms held as arrays, each hashing.Chunk made
+    when it is read (Distribution = histogram / length, as chunkify_batch
+    computes it).  A backup reports tens of thousands of chunks per run; as
+    arrays they cost the callbacks a few copies instead of an object each
+    (and the cyclic collector nothing)."""
+    __slots__ = ("_dg", "_lens", "_ent", "_hist")
+
+    def __init__(self, dg=b"", lens=None, ent=None, hist=None):
+        self._dg = dg
+        self._lens = np.zeros(0, np.int64) if lens is None else lens
+        self._ent = np.zeros(0, np.float64) if ent is None else ent
+        self._hist = np.zeros((0, 256), np.uint32) if hist is None else hist
+
+    @classmethod
+    def concat(cls, parts):
+        parts = [p for p in parts if len(p)]
+        if len(parts) == 1:
+            return parts[0]
+        if not parts:
+            return cls()
+        return cls(b"".join(p._dg for p in parts), np.concatenate([p._lens for p in parts]),
+                   np.concatenate([p._ent for p in parts]), np.concatenate([p._hist for p in parts]))
+
+    def __len__(self):
+        return len(self._lens)
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return [self[i] for i in range(*k.indices(len(self)))]
+        n = len(self)
+        if k < 0:
+            k += n
+        if not 0 <= k < n:
+            raise IndexError(k)
+        length = int(self._lens[k])
+        return hashing.Chunk(self._dg[32 * k:32 * k + 32], length, float(self._ent[k]),
+                             self._hist[k] / float(max(length, 1)))
+
+    def __repr__(self):
+        return f"ChunkRecords({len(self)} chunks)"
+
+
 @dataclass
 class Object:
     """objects.Object (objects/objects.go:26-36), the fields chunkify fills."""
@@ -285,7 +331,7 @@ class BackupSession:
         n = len(paths)
         arr = (ctypes.c_char_p * max(n, 1))(*[str(p).encode() for p in paths])
         objects = [None] * n
-        pending = {}  # file index -> chunks of its pieces so far (files larger than batch_bytes)
+        pending = {}  # file index -> ChunkRecords of its pieces so far (files larger than batch_bytes)
         self.failed = {}  # file index -> status of the files that could not be read (recordError)
         packs = []
         errors = []
@@ -299,22 +345,20 @@ class BackupSession:
                     pending.pop(i, None)
                     return
                 m = int(f.nchunks)
-                chunks = pending.pop(i, [])
-                if m:
+                parts = pending.pop(i, [])
+                if m:  # copies: the pipeline reuses these buffers once the callback returns
                     cuts = np.ctypeslib.as_array(ctypes.cast(f.cuts, ctypes.POINTER(ctypes.c_uint8)),
                                                  (16 * m,)).view(np.dtype(_lib.CUT_DTYPE_FIELDS))
-                    dg = np.ctypeslib.as_array(f.digests, (32 * m,))
-                    hist = np.ctypeslib.as_array(f.hists, (256 * m,)).reshape(m, 256)
-                    lens = cuts["length"].astype(np.int64)
-                    ent = np.ctypeslib.as_array(f.entropy, (m,)).tolist()  # the device's entropy() per chunk
-                    dist = hist / np.maximum(lens, 1)[:, None].astype(np.float64)
-                    dg = dg.tobytes()
-                    chunks += [hashing.Chunk(dg[32 * k:32 * k + 32], int(lens[k]), ent[k], dist[k])
-                               for k in range(m)]
+                    parts.append(ChunkRecords(
+                        np.ctypeslib.as_array(f.digests, (32 * m,)).tobytes(),
+                        cuts["length"].astype(np.int64),
+                        np.ctypeslib.as_array(f.entropy, (m,)).copy(),  # the device's entropy() per chunk
+                        np.ctypeslib.as_array(f.hists, (256 * m,)).reshape(m, 256).copy()))
                 if int(f.piece) + 1 < int(f.pieces):
-                    pending[i] = chunks
+                    pending[i] = parts
                     return
-                objects[i] = Object(Checksum=bytes(f.checksum), Chunks=chunks, Entropy=float(f.object_entropy))
+                objects[i] = Object(Checksum=bytes(f.checksum), Chunks=ChunkRecords.concat(parts),
+                                    Entropy=float(f.object_entropy))
             except Exception as e:  # noqa: BLE001 - re-raised after the call
                 errors.append(e)
 
@@ -372,4 +416,4 @@ def backup_files(paths, repo: Repository = None, key=None, compression="LZ4", kn
         return s.run(paths, keep_packfiles)
 
 
-__all__ = ["Object", "route", "chunkify_batch", "backup_batch", "BackupSession", "backup_files"]
+__all__ = ["Object", "ChunkRecords", "route", "chunkify_batch", "backup_batch", "BackupSession", "backup_files"]

@@ -41,7 +41,10 @@ done
 timeout -k 10 400 python3 bench.py --workload c4 --steps 3 --warmup 1 --cpu-seconds 10 > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err" || exit 1
 timeout -k 10 400 python3 bench.py --workload c4f --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/bench_c4f.json" 2> "$OUT/bench_c4f.err" || exit 1
 timeout -k 10 500 python3 bench.py --workload c4b --steps 5 --warmup 2 > "$OUT/bench_c4b.json" 2> "$OUT/bench_c4b.err" || exit 1
-for wl in c4 c4f c4b; do cut -c1-160 "$OUT/bench_$wl.json"; done
+for r in 2 3; do  # run-to-run spread of the backup leg (reads from the page cache vary)
+  timeout -k 10 500 python3 bench.py --workload c4b --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_c4b_$r.json" 2> "$OUT/bench_c4b_$r.err" || exit 1
+done
+for wl in c4 c4f c4b c4b_2 c4b_3; do cut -c1-160 "$OUT/bench_$wl.json"; done
 echo "[6] N = 2 ranks rehearsed on one GPU (gloo), parity AND + CPU baseline"
 BENCH_REHEARSE_ONE_GPU=1 timeout -k 10 300 python3 bench.py --gpus 2 --steps 20 --warmup 5 --cpu-threads 16 > "$OUT/bench_n2_rehearsal.json" 2> "$OUT/bench_n2.err" || exit 1
 cut -c1-200 "$OUT/bench_n2_rehearsal.json"
