@@ -690,6 +690,9 @@ def main():
                 with open(pth, "wb") as f:
                     f.write(a.tobytes())
                 paths.append(pth)
+            # the share is on disk before the first pass: its dirty pages written
+            # back now, not by the kernel's flusher during the timed reads
+            os.sync()
             del corpus
             fbatch = chunkers.FileBatch(sum((a.size + 4095) // 4096 * 4096 for a in host_bufs))
 

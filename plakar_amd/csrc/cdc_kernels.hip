@@ -2576,47 +2576,10 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         hipLaunchKernelGGL(k_maskl_probe, dim3((B.total_tasks + kProbeWaves - 1) / kProbeWaves), dim3(kProbeWaves * 64),
                            0, st, B, P, W);
     const dim3 rgrid(B.total_segs > 0 ? (B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG : 1u);
-    // CDC_RESOLVE_PRIO=1 (experiment): k_resolve on a per-device stream of
-    // the greatest priority, joined to the caller's stream by events, so its
-    // workgroups are dispatched ahead of another stream's pending scan.
-    static const bool prio = [] {
-        const char *e = getenv("CDC_RESOLVE_PRIO");
-        return e && atoi(e) == 1;
-    }();
-    hipStream_t rs = st;
-    hipEvent_t ejoin = nullptr;
-    if (prio) {
-        struct PrioStream {
-            std::mutex mu;
-            hipStream_t s = nullptr;
-            hipEvent_t ev[64] = {};
-            uint32_t next = 0;
-        };
-        static PrioStream ps[64];
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return CDC_E_DEVICE;
-        PrioStream &Q = ps[dev & 63];
-        std::lock_guard<std::mutex> lk(Q.mu);
-        if (!Q.s) {
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-                hipStreamCreateWithPriority(&Q.s, hipStreamNonBlocking, hi) != hipSuccess)
-                return CDC_E_DEVICE;
-            for (auto &e : Q.ev)
-                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return CDC_E_DEVICE;
-        }
-        hipEvent_t efork = Q.ev[Q.next++ % 64];
-        ejoin = Q.ev[Q.next++ % 64];
-        if (hipEventRecord(efork, st) != hipSuccess || hipStreamWaitEvent(Q.s, efork, 0) != hipSuccess)
-            return CDC_E_DEVICE;
-        rs = Q.s;
-    }
     if (prof)
-        hipExtLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, rs, nullptr, pr.e2, 0, B, P, W);
+        hipExtLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, nullptr, pr.e2, 0, B, P, W);
     else
-        hipLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, rs, B, P, W);
-    if (prio && (hipEventRecord(ejoin, rs) != hipSuccess || hipStreamWaitEvent(st, ejoin, 0) != hipSuccess))
-        return CDC_E_DEVICE;
+        hipLaunchKernelGGL(k_resolve, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
     if (prof) {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof_live.push_back(pr);
