@@ -25,10 +25,11 @@
 //                 4-bit table, and the sealed subkey (header)
 //   k_blob_pows   one wave per blob: H^1..H^64 (a doubling ladder over the
 //                 lanes) and the 8-bit table of H^64
-//   k_gcm         one wave per 64-KiB piece: AES-256-CTR (T-table in LDS,
-//                 32 bank-conflict-free copies) and GHASH (lane l hashes
-//                 blocks l, l+64, ... by Horner in H^64 with an 8-bit table,
-//                 then multiplies by its own H^e), tag
+//   k_gcm         one wave per 64-KiB piece: AES-256-CTR (two rotated
+//                 T-tables in LDS, 32 bank-conflict-free copies each; rounds
+//                 1-2 partly once per piece) and GHASH (lane l hashes blocks
+//                 l, l+64, ... by Horner in H^64 with an 8-bit table, reduced
+//                 once per block, then multiplies by its own H^e), tag
 //
 // Matches stay inside their 16-KiB segment, so compression ratios are those
 // of LZ4 with a 16-KiB window; any LZ4 decoder reads the frames (the tests
