@@ -251,6 +251,16 @@ typedef struct cdc_backup_file {
     const double *entropy;    /* per chunk (Chunk.Entropy: entropy() with Go's math.Log2) */
     double object_entropy;    /* Object.Entropy: sum of entropy * length in chunk order / size */
     uint32_t piece, pieces;   /* this call's piece of the file (pieces == 1: the whole file) */
+    /* This piece's bytes as read (file offsets [data_offset, data_offset +
+     * data_len)), valid during the callback; NULL when the file failed.  The
+     * piece's chunks cover [data_offset, data_offset + the sum of their
+     * lengths); a piece before the last carries its tail into the next.  For
+     * the Object fields the caller computes from the bytes: ContentType
+     * (mime.TypeByExtension, else mimetype.Detect of the first chunk,
+     * snapshot/backup.go:580, 598-601) and the classifier feed
+     * (cprocessor.Write per chunk, backup.go:577, 605). */
+    const uint8_t *data;
+    uint64_t data_offset, data_len;
 } cdc_backup_file;
 typedef struct cdc_backup_stats {
     uint64_t files, bytes, chunks, new_blobs, new_bytes, encoded_bytes, packfiles, packed_bytes, batches;

@@ -61,7 +61,9 @@ class cdc_backup_file(ctypes.Structure):
                 ("size", ctypes.c_uint64), ("nchunks", ctypes.c_uint64), ("cuts", ctypes.POINTER(cdc_cut)),
                 ("digests", ctypes.POINTER(ctypes.c_uint8)), ("hists", ctypes.POINTER(ctypes.c_uint32)),
                 ("is_new", ctypes.POINTER(ctypes.c_uint8)), ("entropy", ctypes.POINTER(ctypes.c_double)),
-                ("object_entropy", ctypes.c_double), ("piece", ctypes.c_uint32), ("pieces", ctypes.c_uint32)]
+                ("object_entropy", ctypes.c_double), ("piece", ctypes.c_uint32), ("pieces", ctypes.c_uint32),
+                ("data", ctypes.POINTER(ctypes.c_uint8)), ("data_offset", ctypes.c_uint64),
+                ("data_len", ctypes.c_uint64)]
 
 
 class cdc_backup_stats(ctypes.Structure):

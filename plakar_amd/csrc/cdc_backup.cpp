@@ -1030,6 +1030,11 @@ int finish_host(Run &R, size_t k)
                 object_entropy_add(F.ent_acc, F.ent_any, f.entropy, f.cuts, f.nchunks);
             }
             f.is_new = s.is_new.data() + s.file_new0[j];
+            if (u.err == CDC_OK) {  // the piece's bytes in the slot's arena (still held: the slot is not released yet)
+                f.data = s.h_arena + u.arena_off;
+                f.data_offset = u.start;
+                f.data_len = u.len;
+            }
             if (last && err == CDC_OK) {
                 std::memcpy(f.checksum, F.obj, 32);
                 f.object_entropy = F.size ? F.ent_acc / double(F.size) : 0.0;

@@ -320,10 +320,14 @@ class BackupSession:
         self._h = ctypes.c_void_p()
         _lib.check(_lib.lib().cdc_backup_new(int(dev), ctypes.byref(o), ctypes.byref(self._h)), "cdc_backup_new")
 
-    def run(self, paths, keep_packfiles=True):
+    def run(self, paths, keep_packfiles=True, content_type=None):
         """Back up the files: (objects, packfiles, stats), as backup_files.
         A file that cannot be read has no object (None) and its status in
-        self.failed; the others are backed up."""
+        self.failed; the others are backed up.  content_type(path, first_chunk)
+        -> str, when given, fills Object.ContentType from the path and the
+        bytes of the file's first chunk, as chunkify does with
+        mime.TypeByExtension and mimetype.Detect (snapshot/backup.go:580,
+        598-601); the bytes come from the pipeline's own read (no re-read)."""
         import ctypes
         from . import _lib
         if not self._h:
@@ -332,6 +336,7 @@ class BackupSession:
         arr = (ctypes.c_char_p * max(n, 1))(*[str(p).encode() for p in paths])
         objects = [None] * n
         pending = {}  # file index -> ChunkRecords of its pieces so far (files larger than batch_bytes)
+        ctypes_of = {}  # file index -> ContentType (from its first piece)
         self.failed = {}  # file index -> status of the files that could not be read (recordError)
         packs = []
         errors = []
@@ -349,6 +354,9 @@ class BackupSession:
                 if m:  # copies: the pipeline reuses these buffers once the callback returns
                     cuts = np.ctypeslib.as_array(ctypes.cast(f.cuts, ctypes.POINTER(ctypes.c_uint8)),
                                                  (16 * m,)).view(np.dtype(_lib.CUT_DTYPE_FIELDS))
+                    if content_type is not None and int(f.piece) == 0 and f.data:
+                        first = ctypes.string_at(f.data, min(int(cuts["length"][0]), int(f.data_len)))
+                        ctypes_of[i] = content_type(paths[i], first)
                     parts.append(ChunkRecords(
                         np.ctypeslib.as_array(f.digests, (32 * m,)).tobytes(),
                         cuts["length"].astype(np.int64),
@@ -358,7 +366,7 @@ class BackupSession:
                     pending[i] = parts
                     return
                 objects[i] = Object(Checksum=bytes(f.checksum), Chunks=ChunkRecords.concat(parts),
-                                    Entropy=float(f.object_entropy))
+                                    ContentType=ctypes_of.pop(i, ""), Entropy=float(f.object_entropy))
             except Exception as e:  # noqa: BLE001 - re-raised after the call
                 errors.append(e)
 

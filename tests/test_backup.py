@@ -181,3 +181,26 @@ def test_backup_session_reused_across_runs(corpus, tmp_path):
     assert s1["new_blobs"] == s3["new_blobs"] > 0
     assert o2[-1].Checksum == hashlib.sha256(big.read_bytes()).digest()
     assert set(_blobs_of(p3, KEY, True)) == {c.Checksum for o in o3 for c in o.Chunks}
+
+
+def test_backup_content_type_sees_each_files_first_chunk(corpus, tmp_path):
+    """Object.ContentType: chunkify takes mime.TypeByExtension, else
+    mimetype.Detect of the first chunk (snapshot/backup.go:580, 598-601).
+    cdc_backup_file carries the piece's bytes for that; the callback gets
+    exactly the file's first chunk, also for a file that goes in pieces."""
+    paths, files = corpus
+    big = tmp_path / "big.bin"
+    big.write_bytes(random_bytes(20 << 20, 321).tobytes())
+    allp, allf = paths + [str(big)], files + [big.read_bytes()]
+    seen = {}
+
+    def sniff(path, first):
+        seen[path] = first
+        return "application/x-test-%d" % len(first)
+
+    with snapshot.BackupSession(key=KEY, batch_bytes=8 << 20, packers=2) as s:
+        objs, _, _ = s.run(allp, content_type=sniff)
+    for p, b, o in zip(allp, allf, objs):
+        n = o.Chunks[0].Length
+        assert seen[p] == b[:n], p
+        assert o.ContentType == "application/x-test-%d" % n
