@@ -36,6 +36,12 @@
 
 namespace cdc {
 
+// s_sleep count (64 cycles each) between polls of a look-back or ticket wait
+#ifndef CDC_SPIN_SLEEP
+#define CDC_SPIN_SLEEP 1
+#endif
+constexpr int kSpinSleep = CDC_SPIN_SLEEP;
+
 static constexpr uint64_t kNoHit = ~0ull;
 static constexpr uint32_t kRawLaneBytes = 512;  // bytes tested per lane per raw-scan block (C3 +5-8 % over 256)
 static constexpr uint32_t kWarm = 64;           // warm-up bytes (>= W - 1 for any mask)
@@ -1877,7 +1883,7 @@ __device__ __forceinline__ uint64_t wait_granule(const uint64_t *p)
     for (;;) {
         const uint64_t v = readlane64(ld_rlx(p), 0);
         if (v) return v;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(kSpinSleep);
     }
 }
 
@@ -1957,7 +1963,7 @@ __device__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t
             uint64_t s = sw[w];
             if (valid) {
                 while (!s) {
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(kSpinSleep);
                     s = ld_rlx(sg + p);
                 }
             }
@@ -2031,7 +2037,7 @@ __device__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t
     }
 slow_path:  // q - 1's own INCLUSIVE status
     uint64_t sq;
-    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) != 2) __builtin_amdgcn_s_sleep(1);
+    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) != 2) __builtin_amdgcn_s_sleep(kSpinSleep);
     E = uint32_t((sq >> 38) & 0xFFFFFFu);
     O = sq & ((1ull << 38) - 1);
 }
@@ -2184,7 +2190,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                         if (r != cur) {  // entered a later segment: its published speculative chain
                             uint64_t xr;
                             while (!((xr = readlane64(ld_rlx(W.xg + base + r), 0)) & kXNodes))
-                                __builtin_amdgcn_s_sleep(1);
+                                __builtin_amdgcn_s_sleep(kSpinSleep);
                             cur = uint32_t(r);
                             cns = uint32_t((xr >> 55) & 0x7Fu);
                             cX = x_dec(xr);
@@ -2301,7 +2307,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     // ---- the buffer's last segment: the result row, or the sequential fallback
     if (fb || __hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         for (uint32_t p = lane; p < q; p += 64)
-            while ((ld_rlx(sgb + p) >> 62) != 2) __builtin_amdgcn_s_sleep(1);
+            while ((ld_rlx(sgb + p) >> 62) != 2) __builtin_amdgcn_s_sleep(kSpinSleep);
         if (__hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || fb) {
             resolve_sequential<kSkip>(C, P, D);
             return;
