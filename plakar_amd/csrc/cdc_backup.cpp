@@ -45,6 +45,7 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <set>
 #include <new>
 #include <string>
 #include <thread>
@@ -320,7 +321,7 @@ struct Run {
     std::vector<uint32_t> batch_of;  // per unit
     uint32_t next_read = 0;        // the next unit to read (guarded by mu)
     uint32_t reading = 0;          // reads in progress (guarded by mu)
-    std::deque<uint32_t> hash_q;   // units read, not yet hashed, in unit order (guarded by mu)
+    std::set<uint32_t> hash_q;     // units read, not yet hashed, in unit order (guarded by mu)
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
@@ -502,12 +503,12 @@ void reader_main(Run &R)
         bool is_read = false;
         {
             std::unique_lock<std::mutex> lk(R.mu);
-            size_t h = 0;
+            auto h = R.hash_q.end();
             R.cv.wait(lk, [&] {
                 if (R.status.load() != CDC_OK) return true;
                 if ((is_read = read_ready_locked(R))) return true;
-                for (h = 0; h < R.hash_q.size(); ++h)
-                    if (hash_ready_locked(R, R.hash_q[h])) return true;
+                for (h = R.hash_q.begin(); h != R.hash_q.end(); ++h)
+                    if (hash_ready_locked(R, *h)) return true;
                 return R.next_read >= R.units.size() && R.reading == 0 && R.hash_q.empty();
             });
             if (R.status.load() != CDC_OK) break;
@@ -528,9 +529,9 @@ void reader_main(Run &R)
                 u.err = F.err;
                 u.start = u.piece ? F.next_start : 0;
                 u.len = u.err == CDC_OK ? u.ne - u.start : 0;
-            } else if (h < R.hash_q.size()) {
-                i = R.hash_q[h];
-                R.hash_q.erase(R.hash_q.begin() + std::ptrdiff_t(h));
+            } else if (h != R.hash_q.end()) {
+                i = *h;
+                R.hash_q.erase(h);
             } else {
                 break;  // every unit read and hashed
             }
@@ -558,7 +559,7 @@ void reader_main(Run &R)
                 --R.reading;
                 // hashes go in unit order (batch order, largest file first),
                 // not in the order reads end: a large file's read ends late
-                R.hash_q.insert(std::upper_bound(R.hash_q.begin(), R.hash_q.end(), i), i);
+                R.hash_q.insert(i);
             }
             R.cv.notify_all();
             continue;
