@@ -204,3 +204,27 @@ def test_backup_content_type_sees_each_files_first_chunk(corpus, tmp_path):
         n = o.Chunks[0].Length
         assert seen[p] == b[:n], p
         assert o.ContentType == "application/x-test-%d" % n
+
+
+def test_backup_many_small_files_rotate_every_slot(tmp_path):
+    """Thousands of files over many more batches than the pipeline has slots
+    (each slot is claimed, released and claimed again many times; reads run
+    ahead of the object hashes): every object and chunk as chunkify gives
+    them, every blob packed once."""
+    rng = np.random.default_rng(77)
+    sizes = rng.integers(0, 48 << 10, size=2500)
+    files, paths = [], []
+    for i, n in enumerate(sizes):
+        b = random_bytes(int(n), 5000 + i).tobytes() if i % 7 else b"dup-%d" % (i % 3)
+        p = tmp_path / f"s{i:05d}"
+        p.write_bytes(b)
+        files.append(b)
+        paths.append(str(p))
+    objs, packs, st = snapshot.backup_files(paths, key=KEY, compression="LZ4", packers=4, readers=8,
+                                            batch_bytes=1 << 20)
+    assert st["batches"] > 20 and st["files"] == len(files)
+    for i, (o, b) in enumerate(zip(objs, files)):
+        assert o.Checksum == hashlib.sha256(b).digest(), i
+        assert sum(c.Length for c in o.Chunks) == len(b), i
+    want = {c.Checksum for o in objs for c in o.Chunks}
+    assert set(_blobs_of(packs, KEY, True)) == want and st["new_blobs"] == len(want)
