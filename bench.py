@@ -630,7 +630,7 @@ def main():
         # value found, as a host that does not set it would run).
         os.environ["BENCH_GPU_MAX_HW_QUEUES_GIVEN"] = os.environ.get("GPU_MAX_HW_QUEUES", "")
         if os.environ.get("BENCH_KEEP_HW_QUEUES") != "1":
-            os.environ["GPU_MAX_HW_QUEUES"] = "8"
+            os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BENCH_HW_QUEUES", "8")
 
     import torch
     import torch.distributed as dist
