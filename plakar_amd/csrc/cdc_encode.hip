@@ -1130,33 +1130,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t gcm_rsrc(uint64_t base, uint64
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, int(n), 0x00020000);
 }
 
-#if defined(GCM_ONE_ROW) && defined(GCM_ONE_ROW_12)
-constexpr uint32_t kGcmWaves = 12, kGcmRows = 1;
-#elif defined(GCM_ONE_ROW)
-constexpr uint32_t kGcmWaves = 16, kGcmRows = 1;  // one row per step, four waves per SIMD
-#else
+// One row per step with 16 waves (12 VGPRs spilled) and one row with 12 waves
+// were 1 % and 19 % slower (profiles/r04_gcm_ab.txt, call 5).
 constexpr uint32_t kGcmWaves = 12;  // one workgroup per CU (LDS: the 64-KiB table), three waves per SIMD
 constexpr uint32_t kGcmRows = 2;    // rows of 64 blocks per step (their AES interleaved)
-#endif
 
-#ifdef GCM_V1
-// LDS of a GCM workgroup.  The T-table in 64 copies, entry e of copy c at
-// byte 256 e + 4 c: lane l reads copy l, so its address is ONE v_perm of the
-// state word and the lane's offset (byte e in bits 8-15, 4 l in bits 0-7), and
-// the 32 lanes of each ds_read_b32 group hit 32 distinct banks whatever the
-// state bytes.  The S-box of the last round is byte 2 of the same entry.
-// rem8: the reduction of the 8 bits a GHASH step shifts out.
-struct GcmLds {
-    uint32_t te[256 * 64];
-    uint64_t rem8[256];
-    struct PerWave {
-        uint32_t rk[60];
-        G128 th[16];
-        G128 t64[256];
-        uint4 stage[64 * kGcmRows];
-    } w[kGcmWaves];
-};
-#else
 // LDS of a GCM workgroup.  Two T-tables, A = Te0 and B = Te0 rotated right by
 // 8 bits, 32 copies each, in one 256-byte row per entry: A's copy c at byte
 // 256 e + 4 c, B's at 256 e + 128 + 4 c.  A ds_read_b32 serves its lanes in
@@ -1175,7 +1153,6 @@ struct GcmLds {
         uint4 stage[64 * kGcmRows];
     } w[kGcmWaves];
 };
-#endif
 
 // Address of state byte k of word w in the 64-copy table.
 __device__ __forceinline__ uint32_t te_addr(uint32_t laneoff, uint32_t w, uint32_t k)
@@ -1188,62 +1165,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-#ifdef GCM_V1
-// N independent blocks at once (their table lookups interleave: more LDS
-// reads in flight per wave).
-template <int N>
-__device__ __forceinline__ void aes256_blocks_lds(const GcmLds::PerWave &PW, const char *te, uint32_t laneoff,
-                                                  uint32_t (&st)[N][4])
-{
-    const uint32_t *rk = PW.rk;
-    auto T = [&](uint32_t w, uint32_t k) { return *reinterpret_cast<const uint32_t *>(te + te_addr(laneoff, w, k)); };
-    uint32_t s[N][4];
-#pragma unroll
-    for (int n = 0; n < N; ++n)
-        for (int q = 0; q < 4; ++q) s[n][q] = st[n][q] ^ rk[q];
-#pragma unroll
-    for (int r = 1; r < 14; ++r) {
-#pragma unroll
-        for (int n = 0; n < N; ++n) {
-            uint32_t t[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                t[q] = xor3(xor3(T(s[n][q], 3), ror32(T(s[n][(q + 1) & 3], 2), 8), ror32(T(s[n][(q + 2) & 3], 1), 16)),
-                            ror32(T(s[n][(q + 3) & 3], 0), 24), rk[4 * r + q]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) s[n][q] = t[q];
-        }
-    }
-    // last round: S-box bytes (byte 2 of the T entries) gathered by v_perm
-    auto S4 = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-        const uint32_t hi = __builtin_amdgcn_perm(T(a, 3), T(b, 2), 0x0602FFFFu);  // [Sa, Sb, -, -]
-        const uint32_t lo = __builtin_amdgcn_perm(T(c, 1), T(d, 0), 0xFFFF0602u);  // [-, -, Sc, Sd]
-        return (hi & 0xFFFF0000u) | (lo & 0xFFFFu);
-    };
-#pragma unroll
-    for (int n = 0; n < N; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            st[n][q] = S4(s[n][q], s[n][(q + 1) & 3], s[n][(q + 2) & 3], s[n][(q + 3) & 3]) ^ rk[56 + q];
-}
-
-// x * V with V's 8-bit table (byte by byte from the last).
-__device__ __forceinline__ G128 gmul8(G128 x, const G128 *t, const uint64_t *rem8)
-{
-    G128 z = t[uint32_t(x.lo) & 255u];
-#pragma unroll
-    for (int i = 14; i >= 0; --i) {
-        const uint32_t byte = i >= 8 ? uint32_t(x.lo >> (8 * (15 - i))) & 255u : uint32_t(x.hi >> (8 * (7 - i))) & 255u;
-        const uint32_t rem = uint32_t(z.lo) & 255u;
-        z.lo = (z.hi << 56) | (z.lo >> 8);
-        z.hi = (z.hi >> 8) ^ rem8[rem];
-        const G128 e = t[byte];
-        z.hi ^= e.hi;
-        z.lo ^= e.lo;
-    }
-    return z;
-}
-#else
 template <int N>
 __device__ __forceinline__ void aes256_blocks_lds(const GcmLds::PerWave &PW, const char *te, uint32_t laneoff,
                                                   uint32_t (&st)[N][4])
@@ -1369,7 +1290,6 @@ __device__ __forceinline__ void aes256_ctr_lds(const GcmLds::PerWave &PW, const 
             st[n][q] = S4(s[n][q], s[n][(q + 1) & 3], s[n][(q + 2) & 3], s[n][(q + 3) & 3]) ^ rk[56 + q];
 }
 
-#ifndef GCM_STEP_REM
 // x * V with V's 8-bit table, reduced once.  x = sum over its bytes b_i
 // (i = 0: the top byte of hi, GCM's x^0..x^7) of b_i x^(8 i), so x V =
 // sum t[b_i] x^(8 i): each entry shifted right by 8 i bits into a 256-bit
@@ -1414,49 +1334,15 @@ __device__ __forceinline__ G128 gmul8(G128 x, const G128 *t)
                __builtin_amdgcn_alignbit(D[3 + k], D[4 + k], 7);
     return G128{uint64_t(D[0] ^ F[0]) << 32 | (D[1] ^ F[1]), uint64_t(D[2] ^ F[2]) << 32 | (D[3] ^ F[3])};
 }
-#else
-// x * V with V's 8-bit table (byte by byte from the last).  The 8 bits a
-// step shifts out, r, fold back as r * (1 + x^5 + x^6 + x^7) (GCM's
-// reflected 0xE1 || 0^120) into bits 49-63 of the high word: computed, not
-// looked up, so the serial chain through z holds no LDS read.
-__device__ __forceinline__ G128 gmul8(G128 x, const G128 *t)
-{
-    G128 z = t[uint32_t(x.lo) & 255u];
-#pragma unroll
-    for (int i = 14; i >= 0; --i) {
-        const uint32_t byte = i >= 8 ? uint32_t(x.lo >> (8 * (15 - i))) & 255u : uint32_t(x.hi >> (8 * (7 - i))) & 255u;
-        const G128 e = t[byte];
-        const uint32_t r = uint32_t(z.lo) & 255u;
-        const uint32_t u = xor3(r, r << 1, r << 2);  // r * (1 + x + x^2)
-        const uint32_t hh = xor3(uint32_t(z.hi >> 40), r << 17, u << 22);  // high dword of (z.hi >> 8) ^ rem
-        z.lo = (z.hi << 56) | (z.lo >> 8);
-        z.hi = ((uint64_t(hh) << 32) | uint32_t(z.hi >> 8)) ^ e.hi;
-        z.lo ^= e.lo;
-    }
-    return z;
-}
-#endif
-#endif
 
 __device__ __forceinline__ uint32_t be32(uint32_t x) { return __builtin_bswap32(x); }
 
 __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
 {
     __shared__ GcmLds L;
-#ifdef GCM_V1
-    for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x) L.te[i] = g_te0[i >> 6];
-    for (uint32_t r = threadIdx.x; r < 256; r += blockDim.x) {
-        uint64_t x = 0;
-        for (uint32_t b = 0; b < 8; ++b)
-            if (r & (1u << b)) x ^= uint64_t(0xE100u >> (7 - b));
-        L.rem8[r] = x << 48;
-    }
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, laneoff = lane << 2;
-#else
     for (uint32_t i = threadIdx.x; i < 256 * 64; i += blockDim.x)
         L.te[i] = (i & 32u) ? ror32(g_te0[i >> 6], 8) : g_te0[i >> 6];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u, laneoff = (lane & 31u) << 2;
-#endif
     const char *te = reinterpret_cast<const char *>(L.te);
     __syncthreads();
     // Persistent: one workgroup per CU; each wave takes pieces from a counter
@@ -1482,9 +1368,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         // this wave's tables (the previous piece's reads of them are done: the
         // wave barrier at the end of its loop body)
         for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk[i] = K.rk[i];
-#ifndef GCM_V1
         for (uint32_t i = lane; i < 60; i += 64) L.w[wv].rk16[i] = ror32(K.rk[i], 16);
-#endif
         if (lane < 16) L.w[wv].th[lane] = K.th[lane];
         for (uint32_t i = lane; i < 256; i += 64) L.w[wv].t64[i] = K.t64[i];
         __builtin_amdgcn_s_waitcnt(0);
@@ -1497,9 +1381,6 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint32_t m = uint32_t(min<uint64_t>(kPiece, F - p0));  // piece bytes
     const uint32_t nb = (m + 15) / 16;
     const gu8 *pt = reinterpret_cast<const gu8 *>(reinterpret_cast<uintptr_t>(plain_ptr(B, b) + p0));
-#ifdef GCM_LATE_LOADS
-    const bool pt_al = (reinterpret_cast<uintptr_t>(pt) & 15u) == 0;
-#endif
     const uint32_t pt_sh = uint32_t(reinterpret_cast<uintptr_t>(pt) & 3u);
     uint8_t *o = B.out + B.out_off[b] + 60 + uint64_t(k) * (kPiece + 28);
     const uint8_t *dn = B.rnd + 56ull * b + 44;  // data nonce
@@ -1509,12 +1390,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     j0[2] = (uint32_t(dn[8]) << 24 | uint32_t(dn[9]) << 16 | uint32_t(dn[10]) << 8 | dn[11]) ^ k;
     if (lane < 12) o[lane] = uint8_t(j0[lane >> 2] >> (24 - 8 * (lane & 3)));
     uint8_t *ct = o + 12;
-#if !defined(GCM_V1) && !defined(GCM_NO_CTR_PRE)
     const CtrPre cpre = ctr_pre(L.w[wv], te, laneoff, j0);
-#endif
     const G128 *t64 = L.w[wv].t64;
     uint8_t *stage = reinterpret_cast<uint8_t *>(L.w[wv].stage);
-#ifndef GCM_LATE_LOADS
     // The piece's plaintext as dwords from its aligned-down start (block i:
     // dwords 4 i .. 4 i + 4, funnel-shifted by its offset in a dword).  A raw
     // buffer returns 0 past its last dword, so every lane loads without a
@@ -1523,7 +1401,6 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint32_t lastq = (pt_sh + m - 1) >> 2;
     const __amdgpu_buffer_rsrc_t prs = gcm_rsrc(reinterpret_cast<uintptr_t>(pt) - pt_sh, uint64_t(lastq + 1) * 4);
     const bool pt_fast = pt_sh == 0 && (m & 15u) == 0;  // whole aligned blocks: one 16-byte load each
-#endif
     // row j: blocks 64 j + lane (1 KiB of the piece), two rows per step (their
     // AES interleaved); lane: Horner in H^64 over its blocks, in order
     G128 Z = {0, 0};
@@ -1538,7 +1415,6 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             c[u][2] = j0[2];
             c[u][3] = 2 + 64 * (j + u) + lane;
         }
-#ifndef GCM_LATE_LOADS
         uint32_t px[kGcmRows][5];
 #pragma unroll
         for (int u = 0; u < int(kGcmRows); ++u) {
@@ -1558,11 +1434,7 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
                     px[u][q] = __builtin_amdgcn_raw_buffer_load_b32(prs, int32_t(4 * min(uint32_t(4 * i + q), lastq)), 0, 0);
             }
         }
-#endif
-#if defined(GCM_DIAG_NO_AES)
-#elif defined(GCM_V1) || defined(GCM_NO_CTR_PRE)
-        aes256_blocks_lds<kGcmRows>(L.w[wv], te, laneoff, c);
-#else
+#ifndef GCM_DIAG_NO_AES  // build-time diagnostic only: no keystream (timing only)
         {
             uint32_t ctr[kGcmRows];
 #pragma unroll
@@ -1577,27 +1449,8 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             if (i < nb) {
                 const uint32_t bytes = min(16u, m - 16 * i);
                 uint32_t pw[4];
-#ifndef GCM_LATE_LOADS
 #pragma unroll
                 for (int q = 0; q < 4; ++q) pw[q] = be32(__builtin_amdgcn_alignbit(px[u][q + 1], px[u][q], 8 * pt_sh));
-#else
-                if (pt_al && bytes == 16) {
-                    const gu32 *q = reinterpret_cast<const gu32 *>(pt + 16 * i);
-                    for (int k = 0; k < 4; ++k) pw[k] = be32(q[k]);
-                } else if (bytes == 16) {  // aligned dwords + v_alignbit (the last one holds needed bytes)
-                    const gu32 *aw =
-                        reinterpret_cast<const gu32 *>(reinterpret_cast<uintptr_t>(pt + 16 * i) & ~uintptr_t(3));
-                    const uint32_t sh = pt_sh * 8u;
-                    uint32_t x[5];
-                    for (int q = 0; q < 4; ++q) x[q] = aw[q];
-                    x[4] = sh ? aw[4] : 0u;
-                    for (int q = 0; q < 4; ++q) pw[q] = be32(sh ? __builtin_amdgcn_alignbit(x[q + 1], x[q], sh) : x[q]);
-                } else {
-                    uint8_t blk[16];
-                    for (uint32_t q = 0; q < 16; ++q) blk[q] = q < bytes ? pt[16 * i + q] : 0;
-                    gcm_block_words(blk, pw);
-                }
-#endif
                 uint32_t w[4];
                 for (int q = 0; q < 4; ++q) w[q] = c[u][q] ^ pw[q];
                 if (bytes < 16) {  // the keystream past the piece's end is not ciphertext (nor hashed)
@@ -1607,10 +1460,8 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
                     }
                 }
                 cw = make_uint4(be32(w[0]), be32(w[1]), be32(w[2]), be32(w[3]));
-#if defined(GCM_DIAG_NO_GHASH)
+#ifdef GCM_DIAG_NO_GHASH  // build-time diagnostic only: no multiply by H^64 (timing only)
                 Z = gx(Z, G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
-#elif defined(GCM_V1)
-                Z = gx(gmul8(Z, t64, L.rem8), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
 #else
                 Z = gx(gmul8(Z, t64), G128{uint64_t(w[0]) << 32 | w[1], uint64_t(w[2]) << 32 | w[3]});
 #endif
@@ -1620,14 +1471,6 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
         }
         __builtin_amdgcn_wave_barrier();
         const uint32_t row_bytes = min(1024u * kGcmRows, m - 1024 * j);
-#ifdef GCM_BYTE_STORE
-        // the rows' ciphertext through LDS: 32 coalesced byte stores of 64 bytes
-#pragma unroll
-        for (uint32_t q = 0; q < 16 * kGcmRows; ++q) {
-            const uint32_t x = 64 * q + lane;
-            if (x < row_bytes) ct[1024 * j + x] = stage[x];
-        }
-#else
         // the rows' ciphertext through LDS: the bytes up to the first aligned
         // dword of the destination, then 8 coalesced dword stores (each dword
         // funnel-shifted from two of the stage's), then the last 0-3 bytes
@@ -1645,7 +1488,6 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
             if (lane < hb) dst[lane] = stage[lane];
             if (lane < tb) dst[hb + 4 * nd + lane] = stage[hb + 4 * nd + lane];
         }
-#endif
         __builtin_amdgcn_wave_barrier();
     }
     if (cnt) {
