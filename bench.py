@@ -627,7 +627,8 @@ def main():
         # before the HIP runtime starts.
         # The GPU box exports HIP's default of 4; the line records the value
         # found and the one applied (BENCH_KEEP_HW_QUEUES=1 measures with the
-        # value found, as a host that does not set it would run).
+        # value found, as a host that does not set it would run; BENCH_HW_QUEUES
+        # picks another count: 16 measured the same as 8, profiles/r04_c4b_hwq_ab.txt).
         os.environ["BENCH_GPU_MAX_HW_QUEUES_GIVEN"] = os.environ.get("GPU_MAX_HW_QUEUES", "")
         if os.environ.get("BENCH_KEEP_HW_QUEUES") != "1":
             os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("BENCH_HW_QUEUES", "8")
