@@ -208,15 +208,28 @@ __device__ __forceinline__ G128 gmul4(G128 x, const TAB &t)
 // a * b bit by bit (SP 800-38D Algorithm 1), for a per-lane multiplier.
 __device__ G128 gmul_bits(G128 a, G128 b)
 {
-    G128 z = {0, 0}, v = b;
-    for (int i = 0; i < 128; ++i) {
-        const uint64_t bit = i < 64 ? (a.hi >> (63 - i)) & 1 : (a.lo >> (127 - i)) & 1;
-        if (bit) z = gx(z, v);
-        const uint64_t r = (v.lo & 1) ? 0xE100000000000000ull : 0;
-        v.lo = (v.lo >> 1) | (v.hi << 63);
-        v.hi = (v.hi >> 1) ^ r;
+    // branch-free: the bit of a as a sign mask (v_ashrrev), z ^= v & mask and
+    // the reduction's 0xE1 as one v_bitop3 each, v shifted by v_alignbit
+    uint32_t z[4] = {0, 0, 0, 0};
+    uint32_t v[4] = {uint32_t(b.hi >> 32), uint32_t(b.hi), uint32_t(b.lo >> 32), uint32_t(b.lo)};
+    const uint32_t aw[4] = {uint32_t(a.hi >> 32), uint32_t(a.hi), uint32_t(a.lo >> 32), uint32_t(a.lo)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t w = aw[k];
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) {
+            const uint32_t m = uint32_t(int32_t(w) >> 31);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[q] = __builtin_amdgcn_bitop3_b32(z[q], v[q], m, 0x78);  // z ^ (v & m)
+            w <<= 1;
+            const uint32_t r = uint32_t(int32_t(v[3] << 31) >> 31);  // v's last bit as a mask
+            v[3] = __builtin_amdgcn_alignbit(v[2], v[3], 1);
+            v[2] = __builtin_amdgcn_alignbit(v[1], v[2], 1);
+            v[1] = __builtin_amdgcn_alignbit(v[0], v[1], 1);
+            v[0] = __builtin_amdgcn_bitop3_b32(v[0] >> 1, r, 0xE1000000u, 0x78);  // (v0 >> 1) ^ (r & 0xE1..)
+        }
     }
-    return z;
+    return {uint64_t(z[0]) << 32 | z[1], uint64_t(z[2]) << 32 | z[3]};
 }
 
 __device__ __forceinline__ G128 g_from_words(const uint32_t w[4])
