@@ -481,13 +481,41 @@ def free_port():
         return s.getsockname()[1]
 
 
+def dist_timeout():
+    """Bound on a rank's rendezvous and on each collective (BENCH_DIST_TIMEOUT_S,
+    default 120 s): a rank whose peer died fails instead of waiting forever
+    (a device failure surfaces as an error, never a hang)."""
+    import datetime
+    return datetime.timedelta(seconds=float(os.environ.get("BENCH_DIST_TIMEOUT_S", "120")))
+
+
+def host_sha256_rate(L, mib=128, reps=3):
+    """One host core's SHA-256 rate (GB/s) through the library's cdc_sha256
+    (the reader threads' object hash), best of `reps` over `mib` MiB."""
+    import ctypes
+    import numpy as np
+    buf = np.random.default_rng(7).integers(0, 256, mib << 20, dtype=np.uint8)
+    out = (ctypes.c_uint8 * 32)()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        if L.cdc_sha256(buf.ctypes.data, buf.size, 0, out) != 0:
+            return float("nan")
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    return buf.size / best / 1e9
+
+
 def spawn_ranks(argv, n):
     """`python bench.py --gpus N` with no launcher: start N rank processes of
     this script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous
-    on 127.0.0.1), wait for all of them and return the worst exit status.  The
-    parent never initialises HIP (device_count() does not, on this image); it
-    refuses to run when fewer than N devices are visible (unless every rank is
-    told to share device 0: BENCH_REHEARSE_ONE_GPU=1, or BENCH_CPU_SELFTEST=1)."""
+    on 127.0.0.1) and poll them.  The first rank that exits non-zero ends the
+    run: the others are terminated (SIGTERM, then SIGKILL after 10 s) and its
+    exit status is returned, so one dead rank never leaves the rest blocked in
+    a rendezvous or a collective.  0 when every rank exits 0.  The parent never
+    initialises HIP (device_count() does not, on this image); it refuses to
+    run when fewer than N devices are visible (unless every rank is told to
+    share device 0: BENCH_REHEARSE_ONE_GPU=1, or BENCH_CPU_SELFTEST=1)."""
     import subprocess
     shared = os.environ.get("BENCH_REHEARSE_ONE_GPU") == "1" or os.environ.get("BENCH_CPU_SELFTEST") == "1"
     if not shared:
@@ -500,9 +528,30 @@ def spawn_ranks(argv, n):
                 LOCAL_WORLD_SIZE=str(n))
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
                               env=dict(base, RANK=str(i), LOCAL_RANK=str(i))) for i in range(n)]
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    first_bad = 0
+    while True:
+        running = [p for p in procs if p.poll() is None]
+        bad = [p for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            first_bad = bad[0].returncode
+            r = procs.index(bad[0])
+            print(f"bench.py: rank {r} exited with status {first_bad}; stopping the other ranks", file=sys.stderr)
+            break
+        if not running:
+            return 0
+        time.sleep(0.05)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.time() + 10
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    # a negative status (killed by a signal) maps to a shell-style exit code
+    return first_bad if first_bad > 0 else 128 + (-first_bad)
 
 
 def gather_per_rank(dist, world, value, dev):
@@ -523,9 +572,15 @@ def cpu_selftest(args, world, rank):
     Each rank "chunks" by sleeping; tests/test_dist.py runs it without a
     launcher to check that --gpus N starts N ranks."""
     import torch.distributed as dist
+    fail_rank = os.environ.get("BENCH_SELFTEST_FAIL_RANK")
+    fail_at = os.environ.get("BENCH_SELFTEST_FAIL_AT", "before")
+    if fail_rank == str(rank) and fail_at == "before":
+        sys.exit(3)  # a rank that dies before the rendezvous
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=dist_timeout())
         dist.barrier()
+    if fail_rank == str(rank) and fail_at == "after":
+        sys.exit(3)  # a rank that dies after the rendezvous, while the others are in a collective
     t0 = time.perf_counter()
     time.sleep(0.01 * (1 + rank))
     el = time.perf_counter() - t0
@@ -649,9 +704,9 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if rehearse:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=dist_timeout())
         else:
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=dist_timeout())
 
     def barrier():
         if world > 1:
@@ -907,25 +962,48 @@ def main():
         }
         if host_mode and wl.get("backup") and backup_stats[0]:
             bs = backup_stats[0]
-            # The leg's device bound is the per-chunk SHA-256 (k_chunk_digest,
-            # DESIGN.md 5.9), not the scan: its roofline is the SHA-256 issue
-            # ceiling, every resident SHA lane (256 CUs x 2 workgroups x 128)
-            # finishing a 64-B block per 2.05 us (one round wave per SIMD).
-            # achieved = bytes hashed per digest launch / the launch's average
-            # duration (digest stage events per batch: arena cuts + SHA-256 +
-            # histograms + entropy).
+            # What bounds the leg is read from its own stage split.  The host's
+            # object SHA-256 (objectHasher, snapshot/backup.go:583, 604: one
+            # serial chain per file) runs on the reader threads; its stage
+            # time is their summed hashing time / readers.  Its ceiling is the
+            # readers x one core's SHA-NI rate (measured here, after the timed
+            # region).  The device's side (the per-chunk SHA-256, k_chunk_digest)
+            # is reported beside it with the device-busy fraction.
+            device_kernel = None
             if bs.get("batches") and bs.get("digest_s"):
-                peak = SHA_LANES * 64 / SHA_BLOCK_S / 1e9
+                # SHA-256 issue ceiling: every resident SHA lane (256 CUs x 2
+                # workgroups x 128) finishing a 64-B block per 2.05 us
+                peak_d = SHA_LANES * 64 / SHA_BLOCK_S / 1e9
                 per = bs["digest_s"] / bs["batches"]
-                ach = bs["bytes"] / bs["batches"] / per / 1e9
-                line["roofline"] = dict(bound="issue", kernel="k_chunk_digest (per-chunk SHA-256 + histograms)",
-                                        achieved=round(ach, 1), peak=round(peak, 1), unit="GB/s",
-                                        frac=round(ach / peak, 4), traffic=None,
-                                        kernel_avg_ms=round(per * 1e3, 3),
-                                        algorithmic_bytes_per_launch=int(bs["bytes"] / bs["batches"]),
-                                        note="a launch lasts as long as its longest chunk's serial SHA-256 chain; "
-                                             "a 256-MiB batch holds ~2,400 chunks against 65,536 resident lanes",
-                                        scan=roofline)
+                ach_d = bs["bytes"] / bs["batches"] / per / 1e9
+                device_kernel = dict(bound="issue", kernel="k_chunk_digest (per-chunk SHA-256 + histograms)",
+                                     achieved=round(ach_d, 1), peak=round(peak_d, 1), unit="GB/s",
+                                     frac=round(ach_d / peak_d, 4), kernel_avg_ms=round(per * 1e3, 3),
+                                     algorithmic_bytes_per_launch=int(bs["bytes"] / bs["batches"]),
+                                     chunks_per_batch=int(bs.get("chunks", 0) / bs["batches"]),
+                                     note="a launch lasts as long as its longest chunk's serial SHA-256 chain; a "
+                                          f"{args.backup_batch_mib}-MiB batch holds ~{int(bs.get('chunks', 0) / bs['batches'])} "
+                                          f"chunks against {SHA_LANES} resident lanes")
+            readers = max(1, args.backup_readers)
+            core = host_sha256_rate(L)
+            stage_s = bs["objhash_s"] / readers
+            wall = bs["wall_s"]
+            stages = {"object SHA-256 (readers)": stage_s, "reads (readers)": bs["read_s"] / readers,
+                      "device (calling thread)": bs["device_s"], "packers": bs["pack_s"] / max(1, args.backup_packers)}
+            bound_stage = max(stages, key=stages.get)
+            ach = bs["bytes"] / stage_s / 1e9
+            line["roofline"] = dict(
+                bound="host-sha256", kernel="object SHA-256 on the reader threads (cdc_sha256, x86 SHA extensions; "
+                                            "objectHasher, snapshot/backup.go:583, 604)",
+                achieved=round(ach, 2), peak=round(readers * core, 2), unit="GB/s",
+                frac=round(ach / (readers * core), 4), traffic=None,
+                per_core_GBps=round(core, 3), readers=readers, stage_s=round(stage_s, 4), wall_s=round(wall, 4),
+                stage_over_wall=round(stage_s / wall, 3), device_busy_frac=round(bs["device_s"] / wall, 3),
+                stage_split_s={k: round(v, 4) for k, v in stages.items()}, longest_stage=bound_stage,
+                note="achieved = bytes / (summed object-hash thread time / readers); peak = readers x one core's "
+                     "SHA-NI rate; the stage that takes longest per thread sets the wall (stage_over_wall); "
+                     "device_busy_frac = the calling thread's device time / wall",
+                device_kernel=device_kernel, scan=roofline)
             line["backup_stages"] = dict(
                 {k: (round(v, 4) if isinstance(v, float) else v) for k, v in bs.items()},
                 readers=args.backup_readers, packers=args.backup_packers, batch_mib=args.backup_batch_mib,

@@ -224,7 +224,11 @@ void cdc_packer_free(cdc_packer *p);
  * regular file, shorter than when it was listed) is reported through on_file
  * with status CDC_E_IO and no chunks, and the backup goes on with the others
  * (backupCtx.recordError, snapshot/backup.go:264-267); stats.failed_files
- * counts them.  Returns CDC_OK, or the first failure of the run itself (a
+ * counts them.  A file in pieces that fails in a later piece (it shrank
+ * mid-run) has had its earlier pieces reported with status CDC_OK and their
+ * chunks (and blobs packed); that piece and every later one then come with
+ * status CDC_E_IO and no chunks, and the last piece's call carries no
+ * checksum: the caller drops the partial object (snapshot.BackupSession does).  Returns CDC_OK, or the first failure of the run itself (a
  * device error, a negative status from on_pack). */
 typedef struct cdc_backup_opts {
     cdc_opts chunking;
@@ -276,9 +280,12 @@ typedef struct cdc_backup_stats {
     uint64_t pieces;          /* units through the pipeline (files + extra pieces of large files) */
     uint64_t slot_arena_bytes;  /* pinned arena bytes per slot this run needed (<= batch_bytes + Max) */
     /* GPU_MAX_HW_QUEUES in the process environment at cdc_backup_new (0: unset,
-     * HIP's default of 4).  The pipeline's four streams + Encode's side stream
-     * run independently only with >= 8 hardware queues; with fewer, HIP maps
-     * several streams onto one queue and the stages serialise. */
+     * HIP's default of 4).  The pipeline's eight streams (scans, H2D, two
+     * digest streams, two encoder streams and one side stream per Encode
+     * workspace) run independently only with >= 8 hardware queues; with fewer,
+     * HIP maps several streams onto one queue and the stages serialise
+     * (INTEGRATION.md).  Other streams of the process (torch's, the collector's)
+     * share queues with them even at 8. */
     int32_t hw_queues;
     int32_t streams_serialised;  /* 1 when hw_queues < 8 (or unset) */
 } cdc_backup_stats;
@@ -442,15 +449,12 @@ int cdc_set_debug_mode(int mode);
  * CDC_E_INVALID. */
 int cdc_set_maskl_index_mode(int mode);
 
-/* How a launch group finds its cut points: 0 = the full scan (every byte
- * rolled by k_scan into a candidate index, then k_resolve), 2 = the skip walk
- * (k_walk: each chain step scans only [p + Min, cut], as the reference's
- * Algorithm reads only those bytes), 1 = adaptive (the skip walk while the
- * data's chunks are mostly short of Normal, the full scan otherwise).  Cut
- * points never depend on it.  Initial value from the CDC_WALK_MODE
- * environment variable.  Not a reference interface.  Returns CDC_OK or
- * CDC_E_INVALID. */
-int cdc_set_walk_mode(int mode);
+/* How a launch group resolves its cut points: 1 = in the same launch as the
+ * scan (k_chunk, the default wherever the group needs no MaskL index), 0 =
+ * always by a second launch (k_scan + k_resolve).  Cut points never depend on
+ * it; tests run both.  Initial value from the CDC_RESOLVE_MODE environment
+ * variable.  Not a reference interface.  Returns CDC_OK or CDC_E_INVALID. */
+int cdc_set_resolve_mode(int mode);
 
 /* Adaptive MaskL state of one device (diagnostics, after a device sync):
  * *hint = 1 while the next launch groups build the MaskL index (a recent

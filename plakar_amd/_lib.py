@@ -170,7 +170,7 @@ SIGNATURES = {
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
-    "cdc_set_walk_mode": (ctypes.c_int, [ctypes.c_int]),
+    "cdc_set_resolve_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_backup_run": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_char_p), ctypes.c_int, _P(cdc_backup_opts),
                                       BACKUP_FILE_FN, BACKUP_PACK_FN, ctypes.c_void_p, _P(cdc_backup_stats)]),
     "cdc_backup_new": (ctypes.c_int, [ctypes.c_int, _P(cdc_backup_opts), _P(ctypes.c_void_p)]),

@@ -89,23 +89,24 @@ Global &G()
     return g;
 }
 
+// Resolution mode (cdc_set_resolve_mode; initial value from CDC_RESOLVE_MODE):
+// 1 the scan and the resolution in one launch (k_chunk) wherever the launch
+// group needs no MaskL index, 0 always two launches (k_scan + k_resolve).
+std::atomic<uint32_t> &resolve_mode()
+{
+    static std::atomic<uint32_t> m([] {
+        const char *e = getenv("CDC_RESOLVE_MODE");
+        return e && e[0] == '0' ? 0u : 1u;
+    }());
+    return m;
+}
+
 // MaskL index mode (cdc_set_maskl_index_mode; initial value from CDC_MASKL_INDEX)
 std::atomic<uint32_t> &maskl_index_mode()
 {
     static std::atomic<uint32_t> m([] {
         const char *e = getenv("CDC_MASKL_INDEX");
         return e && (e[0] == '0' || e[0] == '2' || e[0] == '3') ? uint32_t(e[0] - '0') : 1u;
-    }());
-    return m;
-}
-
-// Walk mode (cdc_set_walk_mode; initial value from CDC_WALK_MODE): 0 the full
-// scan + index resolver, 2 the skip walk, 1 adaptive.
-std::atomic<uint32_t> &walk_mode()
-{
-    static std::atomic<uint32_t> m([] {
-        const char *e = getenv("CDC_WALK_MODE");
-        return e && (e[0] == '0' || e[0] == '1' || e[0] == '2') ? uint32_t(e[0] - '0') : 0u;
     }());
     return m;
 }
@@ -266,6 +267,7 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
     W.sg = reinterpret_cast<uint64_t *>(b + pl.off_sg);
     W.flags = reinterpret_cast<uint32_t *>(b + pl.off_flags);
     W.tick = reinterpret_cast<uint32_t *>(b + pl.off_tick);
+    W.tdone = reinterpret_cast<uint32_t *>(b + pl.off_tdone);
     W.gear = gear;
     W.runsL = reinterpret_cast<uint64_t *>(b + pl.off_runsL);
     W.validL = reinterpret_cast<uint32_t *>(b + pl.off_validL);
@@ -285,11 +287,9 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
     std::memset(&B, 0, sizeof(B));
     B.nbufs = uint32_t(n);
     B.final_ = final_ ? 1u : 0u;
-    const uint32_t wm = walk_mode().load(std::memory_order_relaxed);
-    B.skip = wm == 2 ? 1u : 0u;
-    B.total_segs = B.skip ? pl.total_segs_skip : pl.total_segs;
-    B.total_tasks = B.skip ? 0u : pl.total_tasks;
-    B.seg = B.skip ? pl.seg_skip : pl.seg;
+    B.total_segs = pl.total_segs;
+    B.total_tasks = pl.total_tasks;
+    B.seg = pl.seg;
     B.scan_lane = pl.scan_lane;
     B.persist = pl.persist;
     B.scan_wgs = pl.scan_wgs;
@@ -319,6 +319,7 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         B.maskl_hint = ctx->hint_d;
     }
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
+    B.one_launch = resolve_mode().load(std::memory_order_relaxed) == 1 && !B.maskl_index ? 1u : 0u;
     uint32_t segs = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
         BufDesc &D = B.b[i];
@@ -817,10 +818,10 @@ int cdc_set_debug_mode(int mode)
     return CDC_OK;
 }
 
-int cdc_set_walk_mode(int mode)
+int cdc_set_resolve_mode(int mode)
 {
-    if (mode < 0 || mode > 2) return CDC_E_INVALID;
-    walk_mode().store(uint32_t(mode), std::memory_order_relaxed);
+    if (mode < 0 || mode > 1) return CDC_E_INVALID;
+    resolve_mode().store(uint32_t(mode), std::memory_order_relaxed);
     return CDC_OK;
 }
 

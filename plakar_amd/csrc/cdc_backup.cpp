@@ -101,16 +101,22 @@ int read_exact(const char *path, uint8_t *dst, uint64_t off, uint64_t len)
 // Max - 1 bytes before nb) to ne, non-final except the last piece, so every
 // slot's arena stays at most P + Max bytes whatever the file sizes (the
 // reference streams a file through its chunker in the same way,
-// snapshot/backup.go:647-665).  Pieces of one file run in order: piece j is
-// read once piece j - 1's cut list is back.
+// snapshot/backup.go:647-665).  Piece j's own bytes [nb, ne) are read as soon
+// as its slot is free, at a fixed place (Max bytes into its arena space); the
+// carried prefix [next start, nb) (< Max bytes) is read in front of them once
+// piece j - 1's cut list is back.  So a large file's pieces are read ahead
+// like any other unit, and the device waits only for that short prefix.
 struct Unit {
     uint32_t file, piece, pieces;
     uint64_t nb, ne;       // nominal byte range of the file (what the object hash adds)
     uint64_t cap;          // arena bytes reserved (256-B aligned)
-    uint64_t arena_off;
-    uint64_t start = 0, len = 0;  // set by the reader: file bytes [start, start + len) in the arena
-    int err = CDC_OK;             // set by the reader: CDC_E_IO (the file could not be read)
+    uint64_t arena_off;    // the unit's arena space; [nb, ne) is read to fixed_off()
+    uint64_t start = 0, len = 0;  // set by the readers: file bytes [start, start + len) in the arena ...
+    uint64_t data_off = 0;        // ... from data_off (arena_off for a whole file and a first piece)
+    int err = CDC_OK;             // set by the readers: CDC_E_IO (the file could not be read)
 };
+
+uint64_t fixed_off(const Unit &u, uint64_t max_size) { return u.arena_off + (u.piece ? max_size : 0); }
 
 // Per file, shared by its pieces (guarded by Run::mu unless noted).
 struct FileState {
@@ -322,6 +328,8 @@ struct Run {
     uint32_t next_read = 0;        // the next unit to read (guarded by mu)
     uint32_t reading = 0;          // reads in progress (guarded by mu)
     std::set<uint32_t> hash_q;     // units read, not yet hashed, in unit order (guarded by mu)
+    std::set<uint32_t> prefix_q;   // pieces j > 0 whose [nb, ne) is read, not yet their carried prefix (mu)
+    int64_t fail_file = -1, fail_piece = -1;  // CDC_BACKUP_FAIL_PIECE=file:piece (test hook): that read fails
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
@@ -358,7 +366,16 @@ struct Run {
         trace.push_back(Ev{t, what, batch, unit, bytes});
     }
 
-    Run(cdc_backup *b, const char *const *p, int nn) : B(b), o(b->o), paths(p), n(nn) {}
+    Run(cdc_backup *b, const char *const *p, int nn) : B(b), o(b->o), paths(p), n(nn)
+    {
+        if (const char *f = std::getenv("CDC_BACKUP_FAIL_PIECE")) {
+            long a = -1, c = -1;
+            if (std::sscanf(f, "%ld:%ld", &a, &c) == 2) {
+                fail_file = a;
+                fail_piece = c;
+            }
+        }
+    }
 
     void fail(int s)
     {
@@ -465,28 +482,33 @@ void maybe_release(Run &R, Slot &s)
     }
 }
 
-// Reader threads.  Two kinds of task: reading unit after unit, in batch
+// Reader threads.  Three kinds of task: reading unit after unit, in batch
 // order, into its batch's slot (a slot is claimed by the first unit of its
-// batch once the batch kSlots back released it), and hashing a unit that is
-// read (the object checksum, one serial chain per file: a 124-MiB file is
-// ~62 ms on a host core).  A thread takes the next read whenever it can
-// start, else the first hash in unit order that it can start, so the
-// device's input is never queued behind object hashes (when each reader
-// hashed what it had just read, the 16 largest files held all 16 readers for
-// up to 60 ms while the device waited for the next batch:
-// profiles/r04_c4b_trace.txt).  Piece
-// j > 0 of a large file is read once piece j - 1's carried next start is
-// back from the device, and hashed once piece j - 1 is hashed.  A file that
-// cannot be read is marked failed and the run goes on.
+// batch once the batch kSlots back released it); reading a piece's carried
+// prefix once the previous piece's cut list is back; and hashing a unit that
+// is read (the object checksum, one serial chain per file: a 124-MiB file is
+// ~62 ms on a host core).  A thread takes a prefix whenever one can start
+// (the device waits for it), else the next read, else the first hash in unit
+// order that it can start, so the device's input is never queued behind
+// object hashes (when each reader hashed what it had just read, the 16
+// largest files held all 16 readers for up to 60 ms while the device waited
+// for the next batch: profiles/r04_c4b_trace.txt).  Piece j > 0 of a large
+// file is hashed once piece j - 1 is hashed (its own bytes are at a fixed
+// place, so the hash does not wait for its prefix).  A file that cannot be
+// read is marked failed and the run goes on.
 bool read_ready_locked(Run &R)  // the next unit's read can start (R.mu held)
 {
     if (R.next_read >= R.units.size()) return false;
     const uint32_t i = R.next_read, k = R.batch_of[i];
     const Slot &s = R.B->slot[k % kSlots];
-    if (!(s.batch == int(k) || (s.batch < 0 && s.next == int(k)))) return false;
+    return s.batch == int(k) || (s.batch < 0 && s.next == int(k));
+}
+
+bool prefix_ready_locked(Run &R, uint32_t i)  // piece i's carried prefix can be read (R.mu held)
+{
     const Unit &u = R.units[i];
     const FileState &F = R.files[u.file];
-    return u.piece == 0 || F.err != CDC_OK || F.dev_pieces >= u.piece;
+    return F.err != CDC_OK || u.err != CDC_OK || F.dev_pieces >= u.piece;
 }
 
 bool hash_ready_locked(Run &R, uint32_t i)  // unit i's bytes can go into its object hash (R.mu held)
@@ -498,21 +520,35 @@ bool hash_ready_locked(Run &R, uint32_t i)  // unit i's bytes can go into its ob
 void reader_main(Run &R)
 {
     double read_s = 0, hash_s = 0;
+    const uint64_t M = R.o.chunking.max_size;
     for (;;) {
         uint32_t i = 0;
-        bool is_read = false;
+        bool is_read = false, is_prefix = false;
         {
             std::unique_lock<std::mutex> lk(R.mu);
             auto h = R.hash_q.end();
+            auto pq = R.prefix_q.end();
             R.cv.wait(lk, [&] {
                 if (R.status.load() != CDC_OK) return true;
+                for (pq = R.prefix_q.begin(); pq != R.prefix_q.end(); ++pq)
+                    if (prefix_ready_locked(R, *pq)) return (is_prefix = true);
                 if ((is_read = read_ready_locked(R))) return true;
                 for (h = R.hash_q.begin(); h != R.hash_q.end(); ++h)
                     if (hash_ready_locked(R, *h)) return true;
-                return R.next_read >= R.units.size() && R.reading == 0 && R.hash_q.empty();
+                return R.next_read >= R.units.size() && R.reading == 0 && R.hash_q.empty() && R.prefix_q.empty();
             });
             if (R.status.load() != CDC_OK) break;
-            if (is_read) {
+            if (is_prefix) {
+                i = *pq;
+                R.prefix_q.erase(pq);
+                ++R.reading;
+                Unit &u = R.units[i];
+                FileState &F = R.files[u.file];
+                if (u.err == CDC_OK && F.err != CDC_OK) u.err = F.err;  // an earlier piece failed
+                u.start = u.err == CDC_OK ? F.next_start : u.nb;
+                u.len = u.err == CDC_OK ? u.ne - u.start : 0;
+                u.data_off = fixed_off(u, M) - (u.nb - u.start);
+            } else if (is_read) {
                 i = R.next_read++;
                 ++R.reading;
                 const uint32_t k = R.batch_of[i];
@@ -527,8 +563,11 @@ void reader_main(Run &R)
                 Unit &u = R.units[i];
                 FileState &F = R.files[u.file];
                 u.err = F.err;
-                u.start = u.piece ? F.next_start : 0;
-                u.len = u.err == CDC_OK ? u.ne - u.start : 0;
+                // a whole file or a first piece: [0, ne) at arena_off; a later
+                // piece: its own bytes [nb, ne) now, the prefix once known
+                u.start = u.nb;
+                u.len = u.err == CDC_OK ? u.ne - u.nb : 0;
+                u.data_off = fixed_off(u, M);
             } else if (h != R.hash_q.end()) {
                 i = *h;
                 R.hash_q.erase(h);
@@ -541,13 +580,18 @@ void reader_main(Run &R)
         Slot &s = R.B->slot[k % kSlots];
         Unit &u = R.units[i];
         FileState &F = R.files[u.file];
-        uint8_t *dst = s.h_arena + u.arena_off;
-        if (is_read) {
-            R.ev("read", k, i, u.len);
+        uint8_t *fixed = s.h_arena + fixed_off(u, M);  // the unit's own bytes [nb, ne)
+        if (is_read || is_prefix) {
+            // is_read: [nb, ne) (a whole file: [0, size)); is_prefix: the
+            // carried bytes [start, nb) in front of them
+            const uint64_t off = is_read ? u.nb : u.start, n = is_read ? u.len : u.nb - u.start;
+            uint8_t *dst = is_read ? fixed : s.h_arena + u.data_off;
+            R.ev(is_read ? "read" : "read_prefix", k, i, n);
             const auto t0 = Clock::now();
-            const int st = u.err == CDC_OK ? read_exact(R.paths[u.file], dst, u.start, u.len) : CDC_OK;
+            int st = u.err == CDC_OK ? read_exact(R.paths[u.file], dst, off, n) : CDC_OK;
+            if (is_read && R.fail_file == int64_t(u.file) && R.fail_piece == int64_t(u.piece)) st = CDC_E_IO;
             read_s += secs(t0, Clock::now());
-            R.ev("read_end", k, i, u.len);
+            R.ev("read_end", k, i, n);
             {
                 std::lock_guard<std::mutex> lk(R.mu);
                 if (st != CDC_OK) {
@@ -555,11 +599,14 @@ void reader_main(Run &R)
                     u.len = 0;
                     if (F.err == CDC_OK) F.err = st;
                 }
-                if (++s.nread == b.u1 - b.u0) s.read_done = true;
+                // a later piece is read once its prefix is in too
+                const bool whole = is_prefix || u.piece == 0;
+                if (whole && ++s.nread == b.u1 - b.u0) s.read_done = true;
+                if (is_read && u.piece > 0) R.prefix_q.insert(i);
                 --R.reading;
                 // hashes go in unit order (batch order, largest file first),
                 // not in the order reads end: a large file's read ends late
-                R.hash_q.insert(i);
+                if (is_read) R.hash_q.insert(i);
             }
             R.cv.notify_all();
             continue;
@@ -572,9 +619,9 @@ void reader_main(Run &R)
                 go = u.err == CDC_OK && (u.pieces == 1 || F.err == CDC_OK);
             }
             if (go && u.pieces == 1) {
-                cdc::sha256(dst, u.len, F.obj);
+                cdc::sha256(fixed, u.ne, F.obj);
             } else if (go) {  // the bytes this piece adds: [nb, ne) of the file
-                F.sha.update(dst + (u.nb - u.start), size_t(u.ne - u.nb));
+                F.sha.update(fixed, size_t(u.ne - u.nb));
                 if (u.piece + 1 == u.pieces) F.sha.final(F.obj);
             }
         }
@@ -708,7 +755,7 @@ int enqueue_cuts(Run &R, size_t k)
     uint64_t c = 0;
     for (uint32_t j = 0; j < nf; ++j) {
         const Unit &u = R.units[b.u0 + j];
-        dp[j] = s.d_in + u.arena_off;
+        dp[j] = s.d_in + u.data_off;
         s.lens[j] = u.len;  // 0 for a file that failed (no chunk) and for an empty one (one empty chunk)
         caps[j] = u.len / co->min_size + 2;
         s.cut0[j] = c;
@@ -751,7 +798,7 @@ int enqueue_digests(Run &R, size_t k)
     for (uint32_t j = 0; j < nf; ++j) {
         s.h_meta[3 * j] = s.cut0[j];
         s.h_meta[3 * j + 1] = s.lens[j] / R.o.chunking.min_size + 2;
-        s.h_meta[3 * j + 2] = R.units[b.u0 + j].arena_off;
+        s.h_meta[3 * j + 2] = R.units[b.u0 + j].data_off;
     }
     const uint64_t c = s.ncut;
     HIPOK(hipEventRecord(s.ev[3], sd));
@@ -847,7 +894,7 @@ int finish_device(Run &R, size_t k)
             if (s.lens[j]) {
                 const cdc_cut &cc = s.h_cuts[s.cut0[j] + q];
                 std::memcpy(d.b, s.h_dig + 32 * (s.cut0[j] + q), 32);
-                off = u.arena_off + cc.offset;
+                off = u.data_off + cc.offset;
                 len = cc.length;
             } else {
                 std::memcpy(d.b, kEmptySum, 32);
@@ -1032,7 +1079,7 @@ int finish_host(Run &R, size_t k)
             }
             f.is_new = s.is_new.data() + s.file_new0[j];
             if (u.err == CDC_OK) {  // the piece's bytes in the slot's arena (still held: the slot is not released yet)
-                f.data = s.h_arena + u.arena_off;
+                f.data = s.h_arena + u.data_off;
                 f.data_offset = u.start;
                 f.data_len = u.len;
             }

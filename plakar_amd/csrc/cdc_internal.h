@@ -71,8 +71,8 @@ struct Batch {
     uint32_t *maskl_hint;    // mapped host word: set when some task needed the MaskL index
     uint32_t maskl_probe;    // 1: k_maskl_probe runs the selection test (adaptive mode, hint not set)
     uint64_t seg;            // resolution segment length in bytes
-    uint32_t skip;           // 1: the skip walk (k_walk, no scan, no index); 0: k_scan (+ MaskL) + k_resolve
     uint32_t persist;        // 1: k_scan / k_scan_f run scan_wgs persistent workgroups pulling tasks
+    uint32_t one_launch;     // 1: k_chunk, the scan and the resolution in ONE launch (no MaskL index)
     uint32_t scan_wgs;
     BufDesc b[kMaxBufsPerLaunch];
 };
@@ -86,7 +86,11 @@ struct Workspace {
     uint64_t *xg;        // [total_segs] granule: published | node count | speculative exit X_q
     uint64_t *sg;        // [total_segs] granule: LOCAL (conv, cuts) or INCLUSIVE (E, O)
     uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "resolve sequentially"
-    uint32_t *tick;      // [2] workgroup ticket (dispatch order)
+    uint32_t *tick;      // [8] [0] segment ticket, [2] persistent scan task counter, [3..5] k_chunk tier counters
+    // k_chunk: per scan task, 1 once its run records are stored (write-through)
+    // and readable by another workgroup.  xg .. tdone is one contiguous range,
+    // zeroed before every k_chunk launch.
+    uint32_t *tdone;     // [total_tasks]
     const uint64_t *gear;  // 256 entries, device copy
     // MaskL candidate index (same record format as runs), built by k_scan_l
     // only for the scan tasks near a long MaskS-free stretch; validL[task]
@@ -96,11 +100,11 @@ struct Workspace {
 };
 
 struct Plan {
-    uint64_t seg, seg_skip;  // resolution segment length: full-scan mode, skip walk
+    uint64_t seg;            // resolution segment length
     uint32_t scan_lane;
-    uint32_t total_segs, total_segs_skip, total_tasks;
+    uint32_t total_segs, total_tasks;
     uint32_t persist, scan_wgs;
-    size_t off_runs, off_w1_nodes, off_xg, off_sg, off_flags, off_tick, off_runsL, off_validL,
+    size_t off_runs, off_w1_nodes, off_xg, off_sg, off_flags, off_tick, off_tdone, off_runsL, off_validL,
         bytes;
 };
 

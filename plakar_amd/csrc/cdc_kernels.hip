@@ -223,7 +223,6 @@ constexpr uint32_t kTsClkN = kTsClk + 4 * kClkRecs;   // ring counter
 constexpr uint32_t kTsHw = kTsClkN + 1;               // per scan workgroup: XCC_ID << 32 | HW_ID (kDbgTs)
 constexpr uint32_t kTsSlots = kTsHw + 4096;
 constexpr uint32_t kDbgClk = 64;
-constexpr uint32_t kDbgNoJunctionHint = 128;  // k_walk: junction steps by plain next_node_skip() (A/B)
 __device__ uint64_t g_ts[kTsSlots];
 
 __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
@@ -312,6 +311,14 @@ __device__ __forceinline__ uint32_t rec_cnt(uint64_t rec) { return uint32_t(rec 
 __device__ __forceinline__ uint32_t rec_ent(uint64_t rec, uint32_t e)
 {
     return uint32_t(rec >> (kRecCntBits + kRecEntBits * e)) & ((1u << kRecEntBits) - 1);
+}
+
+// A run record: plain for the next launch, or write-through (relaxed agent
+// store, sc1) for walkers of the same launch (k_chunk).
+__device__ __forceinline__ void put_rec(uint64_t *p, uint64_t v, bool wt)
+{
+    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
 }
 
 // Each lane keeps its run's index record in a register (count + the first
@@ -439,7 +446,7 @@ __device__ __forceinline__ void record_l_group(uint64_t f, const uint64_t (&g)[1
     }
 }
 
-template <bool kMaskL, bool kFused>
+template <bool kMaskL, bool kFused, bool kOne = false>
 __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, const Workspace &W, char *s_lds,
                                           const char *tab, uint32_t task, uint32_t lane, uint32_t wave,
                                           uint32_t laneoff);
@@ -523,8 +530,9 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
 }
 
 // One scan task: the 64 lane runs of task `task` (64 * B.scan_lane bytes of
-// one buffer), staged through this wave's LDS slot.
-template <bool kMaskL, bool kFused>
+// one buffer), staged through this wave's LDS slot.  kOne (k_chunk): the
+// records are stored write-through (sc1), for walkers of the same launch.
+template <bool kMaskL, bool kFused, bool kOne>
 __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, const Workspace &W, char *s_lds,
                                           const char *tab, uint32_t task, uint32_t lane, uint32_t wave,
                                           uint32_t laneoff)
@@ -731,10 +739,13 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
         stage(C0{}, t, A, Bv);
         if (t + 1 < TT) stage(C1{}, t + 1, Bv, A);
     }
-    if (s < int64_t(D.len)) (kMaskL ? W.runsL : W.runs)[64ull * D.task_base + seg0 + lane] = rec;
+    if (s < int64_t(D.len)) put_rec((kMaskL ? W.runsL : W.runs) + 64ull * D.task_base + seg0 + lane, rec, kOne);
     if constexpr (kFused) {
-        if (s < int64_t(D.len)) W.runsL[64ull * D.task_base + seg0 + lane] = recL;
-        if (lane == 0) W.validL[task] = 1u;
+        if (s < int64_t(D.len)) put_rec(W.runsL + 64ull * D.task_base + seg0 + lane, recL, kOne);
+        if (lane == 0) {
+            if constexpr (kOne) __hip_atomic_store(W.validL + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else W.validL[task] = 1u;
+        }
     }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 #ifdef CDC_DIAG_WAITS
@@ -902,10 +913,52 @@ struct WalkCtx {
     const uint64_t *gear;   // the 256-entry table in device memory
     const g_u64 *runsL;     // this buffer's MaskL index records (null: no MaskL index)
     const g_u32 *validL;    // per scan task of the buffer: runsL holds its 64 records
-    const lds_char *tab32;  // k_walk: 32-copy table in the MaskS frame (G << fs_sh), v_perm addresses
-    uint32_t laneoff32;     // (lane & 31) << 3
-    mutable uint32_t blocks;  // k_walk: skip_scan blocks of this wave (wave-uniform)
+    // k_chunk (records written by scan waves of the same launch): the buffer's
+    // per-task "records stored" flags, or null when the records were final
+    // before the launch; [dlo, dhi) tasks already seen done (wave-uniform).
+    const g_u32 *tdone;
+    mutable uint32_t dlo, dhi;
 };
+
+// Wait until the scan tasks holding runs [r_lo, r_hi] of the buffer have
+// stored their records (k_chunk), 64 task flags per round trip.  Every task
+// waited on was claimed by a running wave whose scan never waits, so the wait
+// ends.  The records are then read write-through (ld_run).
+__device__ __forceinline__ void wait_runs(const WalkCtx &C, uint32_t t0, uint32_t t1)
+{
+    for (uint32_t b0 = t0; b0 <= t1; b0 += 64) {
+        const uint32_t t = b0 + C.lane;
+        for (;;) {
+            const uint32_t v = t <= t1 ? __hip_atomic_load(C.tdone + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+            if (!__ballot(v == 0u)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    if (t0 <= C.dhi && t1 + 1 >= C.dlo) {  // extend the known range
+        C.dlo = min(C.dlo, t0);
+        C.dhi = max(C.dhi, t1 + 1);
+    } else {
+        C.dlo = t0;
+        C.dhi = t1 + 1;
+    }
+}
+
+template <bool kGate>
+__device__ __forceinline__ void ensure_runs(const WalkCtx &C, uint64_t r_lo, uint64_t r_hi)
+{
+    if constexpr (!kGate) return;
+    const uint32_t t0 = uint32_t(r_lo >> 6), t1 = uint32_t(r_hi >> 6);  // 64 runs per scan task
+    if (t0 >= C.dlo && t1 < C.dhi) return;
+    wait_runs(C, t0, t1);
+}
+
+// Run record q of the buffer (after ensure_runs when gated).
+template <bool kGate>
+__device__ __forceinline__ uint64_t ld_run(const g_u64 *runs, uint64_t q)
+{
+    if constexpr (kGate) return __hip_atomic_load(runs + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return runs[q];
+}
 
 // (A 32-copy table for long raw scans, filled on first use: C3 +2-4 %, C1 -4 %
 // from the 80-KiB workgroups; not kept.)
@@ -1041,13 +1094,15 @@ __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0
 }
 
 // First full-window MaskS candidate in [a, b) from the run index.
+template <bool kGate>
 __device__ __forceinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
     const uint64_t rl = run_of(C, b - 1);
     for (uint64_t r0 = run_of(C, a); r0 <= rl; r0 += 64) {
         const bool in = r0 + C.lane <= rl;
-        const uint64_t rec = in ? C.runs[r0 + C.lane] : 0ull;
+        ensure_runs<kGate>(C, r0, min(rl, r0 + 63));
+        const uint64_t rec = in ? ld_run<kGate>(C.runs, r0 + C.lane) : 0ull;
         bool done;
         const uint64_t h = recs_first(C, P, r0, in, rec, a, b, fz, done);
         if (done) return h;
@@ -1059,6 +1114,7 @@ __device__ __forceinline__ uint64_t index_first_hit(const WalkCtx &C, const DevP
 // every window is full): from the MaskL index for the scan tasks k_scan_l
 // built (64 records per round trip, dense runs rescanned), by a raw scan for
 // the others.
+template <bool kGate>
 __device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
@@ -1066,9 +1122,13 @@ __device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevP
     const uint64_t ra = run_of(C, a), rl = run_of(C, b - 1);
     for (uint64_t r0 = ra & ~63ull; r0 <= rl; r0 += 64) {
         const uint64_t lo = max(a, r0 * C.sl), hi = min(b, (r0 + 64) * C.sl);
-        if (C.validL[r0 >> 6]) {
+        ensure_runs<kGate>(C, r0, r0);  // validL and runsL of task r0 / 64
+        uint32_t vl;
+        if constexpr (kGate) vl = __hip_atomic_load(C.validL + (r0 >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else vl = C.validL[r0 >> 6];
+        if (vl) {
             const bool in = r0 + C.lane >= ra && r0 + C.lane <= rl;
-            const uint64_t rec = in ? C.runsL[r0 + C.lane] : 0ull;
+            const uint64_t rec = in ? ld_run<kGate>(C.runsL, r0 + C.lane) : 0ull;
             bool done;
             const uint64_t h = recs_first(C, P, r0, in, rec, lo, hi, fz, done, true);
             if (done) return h;
@@ -1086,7 +1146,8 @@ __device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevP
 // Common case in ONE global round trip: every lane issues, together, its
 // truncated-window byte, the candidate count of one index block and two
 // entries of the first two blocks.
-__device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
+template <bool kGate>
+__device__ __forceinline__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
 {
     const uint64_t E = C.len, r = E - p;
     if (r <= P.min_size) return C.final_ ? E : kUndet;
@@ -1123,7 +1184,8 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
     uint32_t byte = 0;
     uint64_t rec = 0;
     if (tvalid) byte = as_space<const g_u8>(C.ub)[tpos];
-    if (rin) rec = C.runs[r0 + j];
+    if (has_s) ensure_runs<kGate>(C, r0, min(rl, r0 + 63));
+    if (rin) rec = ld_run<kGate>(C.runs, r0 + j);
     // ---- truncated window [fz, fz + W - 1)
     uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim, byte);
     if (h != kNoHit) return h + P.cut_adj;
@@ -1133,387 +1195,17 @@ __device__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
         h = recs_first(C, P, r0, rin, rec, full0, s_end, fz, done);
         if (done) return h + P.cut_adj;
         if (r0 + 64 <= rl) {
-            h = index_first_hit(C, P, (r0 + 64) * C.sl, s_end, fz);
+            h = index_first_hit<kGate>(C, P, (r0 + 64) * C.sl, s_end, fz);
             if (h != kNoHit) return h + P.cut_adj;
         }
     }
     // ---- MaskL region [p + Normal, p + n): the MaskL index, or a raw scan
     const uint64_t l_lo = max(norm_end, full0);
     if (l_lo < lim) {
-        h = maskl_first_hit(C, P, l_lo, lim, fz);
+        h = maskl_first_hit<kGate>(C, P, l_lo, lim, fz);
         if (h != kNoHit) return h + P.cut_adj;
     }
     return clipped ? kUndet : p + n;
-}
-
-// ---------------------------------------------------------------------------
-// Skip walk (k_walk): next(p) from the bytes alone, no candidate index.
-//
-// The reference's Algorithm never reads [p, p + Min): it resets fp at
-// p + Min and stops at the first hit.  On random data with the default sizes a
-// chunk is ~96 KiB and the first hit lies ~32 KiB after p + Min, so a walker
-// that scans only [p + Min, cut] touches about a third of the bytes that the
-// full scan (k_scan) rolls, at the price of a sequential chain per resolution
-// segment (the junction / look-back of k_resolve make that chain parallel
-// across segments).  skip_scan is the wave's block scan: 64 lanes, each
-// rolling its own kSkipLane-byte slice after a 64-byte warm-up (reset at fz,
-// exactly as the reference), one ballot per block of 16 KiB.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kSkipLane = 256;                           // bytes tested per lane per block
-constexpr uint32_t kSkipWarm = 64;                            // warm-up bytes (>= W - 1)
-constexpr uint32_t kSkipGroups = (kSkipLane + kSkipWarm) / 16;  // 16-B groups rolled per lane per block
-
-// Raw buffer resource over [base, base + bytes): reads past the end return 0.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(uint64_t base, uint64_t bytes)
-{
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(base));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(base >> 32));
-    const uint32_t n = __builtin_amdgcn_readfirstlane(uint32_t(bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : bytes));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t(hi) << 32) | lo), 0, int(n),
-                                             0x00020000);
-}
-
-// Exact test of one 16-B group (offsets relative to the block base): fp before
-// the group, its 16 Gear values (MaskS frame); positions below fzr restart
-// the fingerprint at 0; returns the first hit in [tsr, ter) or ~0u, and
-// leaves fp exact after the group.
-template <bool kL>
-__device__ __forceinline__ uint32_t skip_exact(uint64_t &fp, const uint64_t (&g)[16], int32_t gr, int32_t tsr,
-                                               int32_t ter, int32_t fzr, const DevParams &P)
-{
-    uint64_t f = fp;
-    uint32_t hit = ~0u;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int32_t pos = gr + k;
-        f = pos < fzr ? 0ull : (f << 1) + g[k];
-        const uint32_t key = kL ? (__builtin_amdgcn_alignbit(uint32_t(f >> 32), uint32_t(f), P.fm_ws) & P.fm_m)
-                                : __builtin_amdgcn_bitop3_b32(uint32_t(f >> 32), P.fs_hi, uint32_t(f) & P.fs_lo, 0xEA);
-        if (hit == ~0u && key == 0 && pos >= tsr && pos < ter) hit = uint32_t(pos);
-    }
-    fp = f;
-    return hit;
-}
-
-// First position in [lo, hi) (buffer-relative) whose fingerprint, reset to 0
-// at fz <= lo, hits: MaskS (kL = false: the hi-dword filter of k_scan, then
-// the exact test) or MaskL (kL = true: its exact window in the MaskS frame,
-// P.fm_ok).  kNoHit if none.  lo >= Min >= 64, so the warm-up of the first
-// block stays inside the buffer's first 16-byte block.
-//
-// Pipelined over blocks: a lane's 320 bytes of a block (64 B of warm-up + its
-// 256-B slice) are two register halves of 10 groups; while the lane rolls one
-// half of block b, the other half's buffer already takes its next bytes (the
-// second half of b, then the first half of b + 1, issued speculatively: a
-// block holds the first hit with probability ~0.4 on random data, and a
-// wasted prefetch costs only bandwidth).  Only a walk's first block waits for
-// its loads.  (Round 3's version loaded a whole block, then rolled it: every
-// block paid a full load latency.)
-#ifdef CDC_SKIP_V3
-// build-time A/B only: round 3's skip_scan (load a block, then roll it)
-template <bool kL>
-__device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo, uint64_t hi, uint64_t fz)
-{
-    const uint32_t lane = C.lane;
-    const lds_char *tab = C.tab32;
-    const uint32_t laneoff = C.laneoff32;
-    const uint64_t FZ = C.ub + fz, H = C.ub + hi, END = C.ub + C.len;
-    const uint32_t vm = to_vgpr(kL ? P.fm_m : P.fs_hi);
-    const uint32_t lws = P.fm_ws;
-    const int32_t lo_off = int32_t(lane * kSkipLane);
-    uint64_t x = C.ub + lo;
-    while (x < H) {
-        const uint64_t A = x & ~15ull;
-        const uint64_t base = A - kSkipWarm;  // wave-uniform
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, END - base);
-        // this lane's tested range [tsr, ter) and the reset point, relative to base
-        const int32_t xr = int32_t(x - base);
-        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr);
-        const int32_t ter = int32_t(min<uint64_t>(uint64_t(lo_off) + kSkipWarm + kSkipLane, H - base));
-        const int32_t fzr = FZ >= base ? int32_t(FZ - base) : -1;
-        uint4 d[kSkipGroups];
-#pragma unroll
-        for (uint32_t i = 0; i < kSkipGroups; ++i)
-            d[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo_off + int32_t(16 * i), 0, 0));
-        uint64_t gv[2][16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(d[0], k >> 2), k));
-        uint64_t fp = 0;
-        uint32_t hit = ~0u;
-#pragma unroll
-        for (uint32_t i = 0; i < kSkipGroups; ++i) {
-            uint64_t (&cg)[16] = gv[i & 1];
-            uint64_t (&ng)[16] = gv[(i + 1) & 1];
-            const uint4 nx = d[i + 1 < kSkipGroups ? i + 1 : i];
-            const uint64_t f0 = fp;
-            uint32_t acc = 0xFFFFFFFFu;
-#pragma unroll
-            for (int k = 0; k < 16; k += 2) {
-                const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
-                fp = (fp << 1) + cg[k];
-                if (i + 1 < kSkipGroups) ng[k] = lds_gear(tab, a0);
-                const uint32_t k0 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
-                                       : (uint32_t(fp >> 32) & vm);
-                const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
-                fp = (fp << 1) + cg[k + 1];
-                if (i + 1 < kSkipGroups) ng[k + 1] = lds_gear(tab, a1);
-                const uint32_t k1 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
-                                       : (uint32_t(fp >> 32) & vm);
-                acc = umin3(acc, k0, k1);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            const int32_t gr = lo_off + int32_t(16 * i);
-            bool chk = acc == 0 && gr + 16 > tsr && gr < ter;
-            if (i * 16 <= kSkipWarm) {  // the groups that can lie before the reset point
-                if (gr + 16 <= fzr) fp = 0;
-                chk = chk || (gr < fzr && gr + 16 > fzr);
-            }
-            if (chk && hit == ~0u) [[unlikely]] {
-                uint64_t f = f0;
-                hit = skip_exact<kL>(f, cg, gr, tsr, ter, fzr, P);
-                fp = f;
-            }
-        }
-        ++C.blocks;
-        const uint64_t m = __ballot(hit != ~0u);
-        if (m) return base + uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) - C.ub;
-        x = A + 64ull * kSkipLane;
-    }
-    return kNoHit;
-}
-
-#else
-// First position in [lo, hi) (buffer-relative) whose fingerprint, reset to 0
-// at fz <= lo, hits: MaskS (kL = false: the hi-dword filter of k_scan, then
-// the exact test) or MaskL (kL = true: its exact window in the MaskS frame,
-// P.fm_ok).  kNoHit if none.  lo >= Min >= 64, so the warm-up of the first
-// block stays inside the buffer's first 16-byte block.
-//
-// Pipelined: a lane's 320 bytes of a block (64 B of warm-up + its 256-B
-// slice) are two halves of 10 groups.  The loop runs over halves; while the
-// lane rolls half h (cur), half h + 1 is already in registers or in flight
-// (nxt), and at the end of half h the loads of half h + 2 are issued into
-// cur's registers (the two arrays then swap: 40 moves per half).  Half h + 2
-// of the next block is read speculatively: a block holds the first hit with
-// probability ~0.4 on random data, and a wasted prefetch costs only
-// bandwidth.  Only a walk's first half waits for its loads.  (Round 3's
-// version loaded a whole block, then rolled it: every block paid a full load
-// latency.  A fully unrolled two-half body spilled: the register allocator
-// could not fit the 20 inlined rechecks beside 80 VGPRs of data.)
-template <bool kL>
-__device__ uint64_t skip_scan(const WalkCtx &C, const DevParams &P, uint64_t lo, uint64_t hi, uint64_t fz)
-{
-    static_assert(kSkipGroups == 20 && kSkipWarm == 64 && kSkipLane == 256, "two halves of 10 groups");
-    constexpr uint32_t kHalf = kSkipGroups / 2;
-    const uint32_t lane = C.lane;
-    const lds_char *tab = C.tab32;
-    const uint32_t laneoff = C.laneoff32;
-    const uint64_t H = C.ub + hi, END = C.ub + C.len;
-    const uint32_t vm = to_vgpr(kL ? P.fm_m : P.fs_hi);
-    const uint32_t lws = P.fm_ws;
-    const int32_t lo_off = int32_t(lane * kSkipLane);
-    const uint64_t x0 = C.ub + lo;
-    const uint64_t A0 = x0 & ~15ull, base0 = A0 - kSkipWarm;  // block b's lanes start at A0 + 16 KiB b
-    const uint32_t nblk = uint32_t((H - A0 + 64ull * kSkipLane - 1) / (64ull * kSkipLane));  // hi - lo <= Max
-    const uint32_t nhalf = 2 * nblk;
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(base0, END - base0);  // reads past the buffer return 0
-    const int32_t xr0 = int32_t(x0 - base0);
-    const int32_t fzr0 = int32_t(int64_t(C.ub + fz) - int64_t(base0));  // <= xr0
-    // Half hh's 10 loads (unconditional, so the waits count them: past the
-    // last half the offset lies beyond the resource's range, which returns
-    // zeros without a memory access).  The scheduling barriers keep them
-    // together at this point of the program.
-    auto load_half = [&](uint4 (&d)[kHalf], uint32_t hh) {
-        const uint32_t o = hh < nhalf ? (hh >> 1) * 64u * kSkipLane + uint32_t(lo_off) + 16u * kHalf * (hh & 1u)
-                                      : 0xFFFFFE00u;
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (uint32_t i = 0; i < kHalf; ++i) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, int32_t(o + 16u * i), 0, 0);
-            d[i] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    uint4 cur[kHalf], nxt[kHalf];
-    load_half(cur, 0);
-    load_half(nxt, 1);
-    // (the compiler's waits count the loads in issue order: a group waits for
-    // its own 16 bytes only, the younger loads stay in flight)
-    uint64_t gv[2][16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) gv[0][k] = lds_gear(tab, gear_addr(laneoff, word_of(cur[0], k >> 2), k));
-    uint64_t fp = 0;
-    uint32_t hit = ~0u;
-    for (uint32_t h = 0; h < nhalf; ++h) {
-        const uint32_t b = h >> 1;
-        const int32_t bo = int32_t(b * 64u * kSkipLane);  // block b relative to block 0
-        // this lane's tested range [tsr, ter) and the reset point, relative to its block's base
-        const int32_t tsr = max(lo_off + int32_t(kSkipWarm), xr0 - bo);
-        const int32_t ter = int32_t(min<int64_t>(int64_t(lo_off) + kSkipWarm + kSkipLane, int64_t(H - base0) - bo));
-        const int32_t fzr = fzr0 - bo;  // negative past block 0
-        const int32_t g0 = int32_t(kHalf * (h & 1u));  // this half's first group in the lane's slice
-        if ((h & 1u) == 0) fp = 0;  // a block starts a lane's warm-up
-#pragma unroll
-        for (uint32_t i = 0; i < kHalf; ++i) {
-            uint64_t (&cg)[16] = gv[i & 1];
-            uint64_t (&ng)[16] = gv[(i + 1) & 1];
-            // the next group's bytes (the next half's first group after the last one;
-            // past the last half they are zeros: harmless gathers)
-            const uint4 nx = i + 1 < kHalf ? cur[i + 1] : nxt[0];
-            const uint64_t f0 = fp;
-            uint32_t acc = 0xFFFFFFFFu;
-#pragma unroll
-            for (int k = 0; k < 16; k += 2) {
-                const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
-                fp = (fp << 1) + cg[k];
-                ng[k] = lds_gear(tab, a0);
-                const uint32_t k0 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
-                                       : (uint32_t(fp >> 32) & vm);
-                const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
-                fp = (fp << 1) + cg[k + 1];
-                ng[k + 1] = lds_gear(tab, a1);
-                const uint32_t k1 = kL ? (__builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vm)
-                                       : (uint32_t(fp >> 32) & vm);
-                acc = umin3(acc, k0, k1);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            const int32_t gr = lo_off + 16 * (g0 + int32_t(i));
-            bool chk = acc == 0 && gr + 16 > tsr && gr < ter;
-            if (g0 == 0 && i * 16 <= kSkipWarm) {  // the groups that can lie before the reset point
-                if (gr + 16 <= fzr) fp = 0;
-                chk = chk || (gr < fzr && gr + 16 > fzr);
-            }
-            if (chk && hit == ~0u) [[unlikely]] {
-                uint64_t f = f0;
-                hit = skip_exact<kL>(f, cg, gr, tsr, ter, fzr, P);
-                fp = f;
-            }
-        }
-        // the two halves swap; half h + 2 goes into the registers of half h
-#pragma unroll
-        for (uint32_t i = 0; i < kHalf; ++i) {
-            const uint4 t = cur[i];
-            cur[i] = nxt[i];
-            nxt[i] = t;
-        }
-        load_half(nxt, h + 2);
-        if (h & 1u) {  // a block ends: the wave's first hit, if any
-            ++C.blocks;
-            const uint64_t m = __ballot(hit != ~0u);
-            if (m)
-                return base0 + uint64_t(bo) +
-                       uint32_t(__builtin_amdgcn_readlane(int(hit), __ffsll((unsigned long long)m) - 1)) - C.ub;
-        }
-    }
-    return kNoHit;
-}
-
-#endif  // CDC_SKIP_V3
-
-// next_node() from the bytes alone (k_walk): the same window rules, every
-// candidate found by skip_scan (the truncated window included: skip_scan
-// restarts the fingerprint at fz).
-__device__ uint64_t next_node_skip(const WalkCtx &C, const DevParams &P, uint64_t p)
-{
-    const uint64_t E = C.len, r = E - p;
-    if (r <= P.min_size) return C.final_ ? E : kUndet;
-    uint64_t n, norm = P.normal_size, lim;
-    bool clipped = false;
-    if (C.final_) {
-        if (r >= P.max_size) {
-            n = P.max_size;
-        } else {
-            n = r;
-            if (r <= P.normal_size) norm = r;
-        }
-        lim = p + n;
-    } else {
-        n = P.max_size;
-        lim = p + n;
-        if (lim > E) {
-            lim = E;
-            clipped = true;
-        }
-    }
-    const uint64_t fz = p + P.min_size;
-    const uint64_t norm_end = p + norm;
-    const uint64_t s_end = min(norm_end, lim);
-    if (fz < s_end) {
-        const uint64_t h = skip_scan<false>(C, P, fz, s_end, fz);
-        if (h != kNoHit) return h + P.cut_adj;
-    }
-    const uint64_t l_lo = max(norm_end, fz);
-    if (l_lo < lim) {
-        const uint64_t h = P.fm_ok ? skip_scan<true>(C, P, l_lo, lim, fz)
-                                   : raw_first_hit(C, l_lo, lim, fz, P.ml_lo, P.ml_hi);
-        if (h != kNoHit) return h + P.cut_adj;
-    }
-    return clipped ? kUndet : p + n;
-}
-
-// A junction step of the skip walk (k_walk, phase B) from x, given the
-// speculative chain of the segment holding x (node i in lane i of cv, cns
-// nodes, cX the node after the last): the speculative walk already scanned
-// [p_k + Min, h] for its node p_k <= x < p_{k+1} = h + cut_adj and found no
-// full-window MaskS hit before h.  When h was such a hit (full window relative
-// to p_k, inside p_k's MaskS region) and lies at or past x's first
-// full-window position, it is x's next node too unless x's own truncated
-// window [x + Min, x + Min + W - 1) hits: one 49-byte check instead of a
-// scan.  When x is too close to p_{k+1} for that, only [x + Min, p_{k+1} + Min
-// + W - 1) is scanned: past it the speculative walk's next interval
-// [p_{k+1} + Min + W - 1, p_{k+2} - cut_adj) is hit-free, so without a hit the
-// answer is p_{k+2}.  Anything else takes the plain next_node_skip().
-__device__ uint64_t next_skip_junction(const WalkCtx &C, const DevParams &P, uint64_t x, uint64_t cv, uint32_t cns,
-                                       uint64_t cX)
-{
-    const uint64_t E = C.len, r = E - x;
-    const uint64_t m = __ballot(C.lane < cns && cv <= x);
-    if (r <= P.min_size || !m) return next_node_skip(C, P, x);
-    const int kk = 63 - int(__builtin_clzll(m));
-    const uint64_t pk = readlane64(cv, kk);
-    const uint64_t pk1 = kk + 1 < int(cns) ? readlane64(cv, kk + 1) : cX;
-    const uint64_t pk2 = kk + 2 < int(cns) ? readlane64(cv, kk + 2) : kk + 1 < int(cns) ? cX : kUndet;
-    // x's MaskS region [x + Min, s_end), as next_node_skip() bounds it
-    uint64_t norm = P.normal_size, lim;
-    if (C.final_) {
-        const uint64_t n = r >= P.max_size ? P.max_size : r;
-        if (r < P.max_size && r <= P.normal_size) norm = r;
-        lim = x + n;
-    } else {
-        lim = min(x + P.max_size, E);
-    }
-    const uint64_t s_end = min(x + norm, lim);
-    const uint64_t wm1 = P.win - 1;
-    // a node decided by a full-window MaskS hit of its predecessor q (not a
-    // truncated-window hit, not MaskL, not a forced or end-of-buffer cut)
-    auto full_hit_of = [&](uint64_t q, uint64_t nxt) {
-        return nxt != kUndet && nxt < E && nxt > q && nxt - P.cut_adj >= q + P.min_size + wm1 &&
-               nxt - P.cut_adj < q + P.normal_size;
-    };
-    if (!(x < pk1 && full_hit_of(pk, pk1))) return next_node_skip(C, P, x);
-    const uint64_t h = pk1 - P.cut_adj;
-    const uint64_t fz = x + P.min_size;
-    if (h >= fz + wm1 && h < s_end) {  // only x's truncated window is new
-        const uint32_t j = C.lane;
-        const uint64_t tpos = fz + j;
-        const uint32_t byte = (j + 1 < P.win && tpos < lim) ? as_space<const g_u8>(C.ub)[tpos] : 0u;
-        const uint64_t t = trunc_first_hit(C, P, fz, x + norm, lim, byte);
-        return t != kNoHit ? t + P.cut_adj : pk1;
-    }
-    const uint64_t stop = min(s_end, pk1 + P.min_size + wm1);
-    if (fz < stop) {
-        const uint64_t hh = skip_scan<false>(C, P, fz, stop, fz);
-        if (hh != kNoHit) return hh + P.cut_adj;
-    }
-    if (stop < s_end && full_hit_of(pk1, pk2) && pk2 - P.cut_adj < s_end) return pk2;
-    return next_node_skip(C, P, x);
-}
-
-template <bool kSkip>
-__device__ __forceinline__ uint64_t next_of(const WalkCtx &C, const DevParams &P, uint64_t p)
-{
-    if constexpr (kSkip) return next_node_skip(C, P, p);
-    else return next_node(C, P, p);
 }
 
 // ---------------------------------------------------------------------------
@@ -1539,11 +1231,27 @@ constexpr uint32_t kGRecs = 512;       // run records preloaded per wave
 constexpr uint64_t kGHard = ~1ull;     // successor not decided by the graph
 constexpr uint32_t kGNone = 0xFFFFu;   // not a listed node
 
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
 struct GraphLds {
-    uint64_t rec[kGRecs];        // runs ra .. ra + nr - 1
-    uint64_t bits[kGRecs / 64];  // bit i: run ra + i holds a candidate (dense included)
-    uint64_t node[kGNodes];      // listed nodes, ascending
+    lds_u64 *rec;   // [kGRecs] runs ra .. ra + nr - 1
+    lds_u64 *bits;  // [kGRecs / 64] bit i: run ra + i holds a candidate (dense included)
+    lds_u64 *node;  // [kGNodes] listed nodes, ascending
 };
+constexpr uint32_t kGExtra = kGRecs / 64 + kGNodes;  // words of bits + node
+
+__device__ __forceinline__ lds_u64 *lds_words(void *p)  // a generic pointer to LDS as an LDS pointer
+{
+    return as_space<lds_u64>(uint32_t(reinterpret_cast<uintptr_t>(p)));
+}
+
+__device__ __forceinline__ GraphLds graph_lds(void *rec, void *extra)
+{
+    GraphLds L;
+    L.rec = lds_words(rec);
+    L.bits = lds_words(extra);
+    L.node = L.bits + kGRecs / 64;
+    return L;
+}
 
 // The chunk window next_node() works on for a chunk starting at p (r > Min).
 struct ChunkWin {
@@ -1706,7 +1414,8 @@ __device__ __forceinline__ uint32_t graph_lookup(const Graph &G, uint32_t lane, 
 }
 
 // Build the graph of segment [S0, S1): list, preload, successors.
-__device__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, Graph &G, uint64_t S0, uint64_t S1,
+template <bool kGate>
+__device__ __forceinline__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, Graph &G, uint64_t S0, uint64_t S1,
                             const Batch &B, uint32_t tslot)
 {
     const bool tg = (B.debug & kDbgGraph) && C.lane == 0;
@@ -1717,10 +1426,11 @@ __device__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, G
     const uint64_t rneed = run_of(C, min(C.len, S1 + P.normal_size) - 1);
     const uint32_t nr = uint32_t(min<uint64_t>(rneed - ra + 1, kGRecs));
     uint64_t recs[kGRecs / 64];
+    ensure_runs<kGate>(C, ra, ra + nr - 1);
 #pragma unroll
     for (uint32_t k = 0; k < kGRecs / 64; ++k) {
         const uint32_t i = 64u * k + lane;
-        recs[k] = 64u * k < nr && i < nr ? C.runs[ra + i] : 0ull;
+        recs[k] = 64u * k < nr && i < nr ? ld_run<kGate>(C.runs, ra + i) : 0ull;
     }
     uint32_t n = 1;  // node 0: the segment start (the speculative chain's first node)
     if (lane == 0) L.node[0] = S0;
@@ -1813,9 +1523,9 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.gear = W.gear;
     C.runsL = B.maskl_index ? as_space<const g_u64>(reinterpret_cast<uintptr_t>(W.runsL + 64ull * D.task_base)) : nullptr;
     C.validL = B.maskl_index ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.validL + D.task_base)) : nullptr;
-    C.tab32 = nullptr;
-    C.laneoff32 = 0;
-    C.blocks = 0;
+    C.tdone = B.one_launch ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.tdone + D.task_base)) : nullptr;
+    C.dlo = 0;
+    C.dhi = 0;
     return C;
 }
 
@@ -1943,7 +1653,7 @@ __device__ __forceinline__ uint32_t row_incl_sum32(uint32_t x)
     return x;
 }
 
-__device__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O)
+__device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O)
 {
     uint32_t Fe = q + lane;  // F, lane t < kJ: entering at hi + 1 + t leaves E = Fe with Fo cuts added
     uint64_t Fo = 0;
@@ -2044,12 +1754,12 @@ slow_path:  // q - 1's own INCLUSIVE status
 
 // The sequential walk of a whole buffer (debug mode, lists that overflow):
 // one wave walks next() from offset 0 and writes the cut list and the result row.
-template <bool kSkip>
+template <bool kGate>
 __device__ __forceinline__ void resolve_sequential(const WalkCtx &C, const DevParams &P, const BufDesc &D)
 {
     uint64_t p = 0, idx = 0;
     while (p < C.len) {
-        const uint64_t nx = next_of<kSkip>(C, P, p);
+        const uint64_t nx = next_node<kGate>(C, P, p);
         if (nx == kUndet) break;
         if (C.lane == 0 && idx < D.cap) put_cut(D.out + idx, p, nx - p);
         ++idx;
@@ -2064,24 +1774,19 @@ __device__ __forceinline__ void resolve_sequential(const WalkCtx &C, const DevPa
     }
 }
 
-template <bool kSkip>
+template <bool kGate>
 __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams &P, const Workspace &W, uint32_t g,
-                                                const char *tab, const char *tab32, GraphLds *L)
+                                                const char *tab, GraphLds L)
 {
     const uint32_t b = buf_of_seg(B, g);
     const BufDesc &D = B.b[b];
     WalkCtx C = make_ctx(B, D, W, tab);
-    if constexpr (kSkip) {
-        C.tab32 = as_lds(tab32);
-        C.laneoff32 = (C.lane & 31u) << 3;
-    }
     const uint32_t lane = C.lane, base = D.seg_base, q = g - base;
     const uint64_t seg = B.seg, S0 = uint64_t(q) * seg, segE = S0 + seg, S1 = min(segE, C.len);
     const bool l0 = lane == 0;
     if (l0) dbg_ts(B, kTsRes + 8 * g);
     Graph G;
-    if constexpr (kSkip) G.n = kGNodes + 1;  // no index: every step is next_node_skip()
-    else graph_build(C, P, *L, G, S0, S1, B, kTsRes + 8 * g);
+    graph_build<kGate>(C, P, L, G, S0, S1, B, kTsRes + 8 * g);
     if (l0) dbg_ts(B, kTsRes + 8 * g + 1);
     bool ovf = false;
     // ---- A (phase 0) and B (phase 1).  While the walk stays on listed nodes
@@ -2188,12 +1893,22 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                     if (phase == 1) {
                         const uint64_t r = x / seg;
                         if (r != cur) {  // entered a later segment: its published speculative chain
+                            // (k_chunk waits only for a segment some running wave
+                            // has taken: phase A never waits for a later one, so
+                            // the wait ends; an untaken segment is walked through)
                             uint64_t xr;
-                            while (!((xr = readlane64(ld_rlx(W.xg + base + r), 0)) & kXNodes))
+                            for (;;) {
+                                xr = readlane64(ld_rlx(W.xg + base + r), 0);
+                                if (xr & kXNodes) break;
+                                if (kGate &&
+                                    __hip_atomic_load(W.tick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= base + r)
+                                    break;
                                 __builtin_amdgcn_s_sleep(kSpinSleep);
+                            }
                             cur = uint32_t(r);
-                            cns = uint32_t((xr >> 55) & 0x7Fu);
-                            cX = x_dec(xr);
+                            const bool pub = (xr & kXNodes) != 0;
+                            cns = pub ? uint32_t((xr >> 55) & 0x7Fu) : 0u;
+                            cX = pub ? x_dec(xr) : kUndet;
                             cv = lane < cns ? ld_rlx(W.w1_nodes + size_t(base + r) * kMaxList + lane) : kUndet;
                         }
                         const uint64_t m = __ballot(lane < cns && cv == x);
@@ -2229,12 +1944,8 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 }
                 if (s != kGHard) {
                     nx = s;
-                } else if (kSkip && phase == 1 && !(B.debug & kDbgNoJunctionHint)) {
-                    nx = next_skip_junction(C, P, x, cv, cns, cX);
-                    ni = kGNone;
-                    ++exact;
                 } else {
-                    nx = next_of<kSkip>(C, P, x);
+                    nx = next_node<kGate>(C, P, x);
                     ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
                     ++exact;
                 }
@@ -2298,7 +2009,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
         st_rlx(W.sg + g, kKindIncl | (uint64_t(Eq) << 38) | Oq);
         dbg_ts(B, kTsRes + 8 * g + 4);
         if (!(B.debug & kDbgGraph)) {
-            dbg_ts(B, kTsRes + 8 * g + 5, kSkip ? C.blocks : G.n);
+            dbg_ts(B, kTsRes + 8 * g + 5, G.n);
             dbg_ts(B, kTsRes + 8 * g + 6, exact);
             dbg_ts(B, kTsRes + 8 * g + 7, c2);
         }
@@ -2309,7 +2020,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
         for (uint32_t p = lane; p < q; p += 64)
             while ((ld_rlx(sgb + p) >> 62) != 2) __builtin_amdgcn_s_sleep(kSpinSleep);
         if (__hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || fb) {
-            resolve_sequential<kSkip>(C, P, D);
+            resolve_sequential<kGate>(C, P, D);
             return;
         }
     }
@@ -2321,60 +2032,107 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     }
 }
 
+// Empty buffers have no segment to write their result row.
+__device__ __forceinline__ void write_empty_rows(const Batch &B, uint32_t lane)
+{
+    for (uint32_t i = lane; i < B.nbufs; i += 64) {
+        if (B.b[i].nseg == 0) {
+            B.b[i].res->ncuts = 0;
+            B.b[i].res->consumed = 0;
+            B.b[i].res->status = CDC_OK;
+            B.b[i].res->needed = 0;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B, const DevParams P, const Workspace W)
 {
     __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
-    __shared__ GraphLds s_graph[kWalkWavesPerWG];
+    __shared__ uint64_t s_grec[kWalkWavesPerWG][kGRecs];
+    __shared__ uint64_t s_gx[kWalkWavesPerWG][kGExtra];
     __shared__ uint32_t s_ticket;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(W.tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
     __syncthreads();
-    if (blockIdx.x == 0 && wave == 0) {  // empty buffers have no segment to write their row
-        for (uint32_t i = lane; i < B.nbufs; i += 64) {
-            if (B.b[i].nseg == 0) {
-                B.b[i].res->ncuts = 0;
-                B.b[i].res->consumed = 0;
-                B.b[i].res->status = CDC_OK;
-                B.b[i].res->needed = 0;
-            }
-        }
-    }
+    if (blockIdx.x == 0 && wave == 0) write_empty_rows(B, lane);
     const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(s_ticket)) * kWalkWavesPerWG + wave;
     if (g < B.total_segs)
-        resolve_segment<false>(B, P, W, g, reinterpret_cast<const char *>(s_tab), nullptr, &s_graph[wave]);
+        resolve_segment<false>(B, P, W, g, reinterpret_cast<const char *>(s_tab), graph_lds(s_grec[wave], s_gx[wave]));
 }
 
-// The skip walk: k_resolve's phases over next_node_skip(), no scan kernel
-// before it (B.skip; the launch zeroes the granules with one memset).
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_walk(const Batch B, const DevParams P, const Workspace W)
+// ---------------------------------------------------------------------------
+// k_chunk: the scan and the chain resolution of a launch group in ONE launch
+// (the launch group needs no MaskL index).  Workgroups as k_scan's (12 waves,
+// one per CU); every wave first scans, then resolves:
+//
+//   * Scan tasks are claimed, not assigned: the waves of a SIMD finish in age
+//     order (the oldest first: DESIGN.md 5.1, round 4), so wave w of a
+//     workgroup claims from tier w / 4's counter, and tier k holds the k-th
+//     third of the launch group's tasks.  The buffer's first third is then
+//     final when the oldest waves end, the last third when the youngest do.
+//     A wave whose tier is used up claims from the others (a workgroup that
+//     starts late, its CU held by another stream's kernel, finds its tasks
+//     taken).  After its task a wave stores its records write-through, drains
+//     them and raises the task's flag (tdone).
+//   * Resolution segments are claimed in order (W.tick[0]) only once every
+//     scan task is claimed, and k_resolve's phases run on them (issue
+//     priority below the scan, which sets the critical path).  A walker
+//     waits for the flags of the tasks whose records it reads (ensure_runs);
+//     a junction waits for a later segment's speculative chain only if a
+//     running wave has taken that segment.  Every wait is therefore on a
+//     running wave that will not wait on it: no deadlock whatever the
+//     residency (the other stream's kernel may hold any CUs).
+//
+// The segments of the first two thirds are resolved while the younger waves
+// still scan; only the last third's resolution follows the last scan task.
+// The host zeroes xg .. tdone (counters, flags, granules) before the launch.
+// LDS: the scan's 64-KiB shifted Gear table and 12 x 4-KiB slots (a wave's
+// slot then holds its graph's run records), the walkers' 16-KiB table, and
+// 12 x 1,088 B of graph bits and nodes: 141 KiB.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kTiers = 3;
+static_assert(kS2Waves % kTiers == 0, "tiers of whole SIMD rounds");
+static_assert(kGRecs * 8 <= kStageBytes, "a wave's graph records fit its scan slot");
+
+__global__ __launch_bounds__(kS2Waves * 64) void k_chunk(const Batch B, const DevParams P, const Workspace W)
 {
-    // 80 KiB of tables: two workgroups per CU.  Each wave takes its own
-    // ticket (no LDS word for a workgroup ticket: it would push the
-    // workgroup past half the CU's LDS).
-    __shared__ __attribute__((aligned(16))) uint64_t s_tab32[256 * 32];
-    __shared__ uint64_t s_tab[256 * kWCopies];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    uint32_t tk = 0;
-    if (lane == 0) tk = __hip_atomic_fetch_add(W.tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(tk));
-    fill_gear_lds<kWalkWavesPerWG * 64, 32>(s_tab32, W.gear, P.fs_sh);
-    fill_gear_lds<kWalkWavesPerWG * 64, kWCopies>(s_tab, W.gear);
+    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kStageBytes];
+    __shared__ uint64_t s_wtab[256 * kWCopies];
+    __shared__ uint64_t s_gx[kS2Waves][kGExtra];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t laneoff = (lane & 31u) << 3;
+    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, P.fs_sh);
+    fill_gear_lds<kS2Waves * 64, kWCopies>(s_wtab, W.gear);
+    if (blockIdx.x == 0 && wave == 0) write_empty_rows(B, lane);
     __syncthreads();
-    if (blockIdx.x == 0 && wave == 0) {
-        for (uint32_t i = lane; i < B.nbufs; i += 64) {
-            if (B.b[i].nseg == 0) {
-                B.b[i].res->ncuts = 0;
-                B.b[i].res->consumed = 0;
-                B.b[i].res->status = CDC_OK;
-                B.b[i].res->needed = 0;
-            }
+    __builtin_amdgcn_s_setprio(1);
+    const uint32_t T = B.total_tasks, tpt = (T + kTiers - 1) / kTiers;
+    const uint32_t tier = wave / (kS2Waves / kTiers);
+    for (uint32_t k = 0; k < kTiers; ++k) {
+        const uint32_t tr = tier + k < kTiers ? tier + k : tier + k - kTiers;
+        for (;;) {
+            uint32_t i = 0;
+            if (lane == 0) i = __hip_atomic_fetch_add(W.tick + 3 + tr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            i = __builtin_amdgcn_readfirstlane(i);
+            const uint32_t task = tr * tpt + i;
+            if (i >= tpt || task >= T) break;
+            scan_task<false, false, true>(B, P, W, s_lds, s_lds, task, lane, wave, laneoff);
+            drain_stores();
+            if (lane == 0) __hip_atomic_store(W.tdone + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (g < B.total_segs)
-        resolve_segment<true>(B, P, W, g, reinterpret_cast<const char *>(s_tab),
-                              reinterpret_cast<const char *>(s_tab32), nullptr);
+    __builtin_amdgcn_s_setprio(0);
+    const GraphLds L = graph_lds(s_lds + kGearLdsBytes + wave * kStageBytes, s_gx[wave]);
+    for (;;) {
+        uint32_t g = 0;
+        if (lane == 0) g = __hip_atomic_fetch_add(W.tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g >= B.total_segs) break;
+        resolve_segment<true>(B, P, W, g, reinterpret_cast<const char *>(s_wtab), L);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2401,15 +2159,6 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     if (seg < need) seg = need;
     seg = (seg + 15) & ~15ull;
     plan->seg = seg;
-    // Skip-walk segments (k_walk): 8 Min (512 KiB at the defaults), two walker
-    // waves per SIMD on a 1-GiB buffer.  Every step of a walk scans bytes, so a
-    // segment is a trade between chain parallelism and the junction (about 1.4
-    // extra steps per segment on random data).
-    uint64_t smult = 8;
-    uint64_t seg_skip = smult * P.min_size;
-    if (seg_skip < need) seg_skip = need;
-    seg_skip = (seg_skip + 15) & ~15ull;
-    plan->seg_skip = seg_skip;
     // Scan lane length: one scan workgroup per CU (a workgroup holds 112 KiB of
     // LDS), for a grid of at most CUs - 7 workgroups; lane lengths are
     // multiples of 256 B (odd multiples of 128 B ran slower), so 1 GiB takes
@@ -2467,17 +2216,14 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     }
     plan->scan_lane = lane;
     const uint64_t task_bytes = 64ull * lane;
-    uint64_t segs = 0, segs_skip = 0, tasks = 0;
+    uint64_t segs = 0, tasks = 0;
     for (int i = 0; i < nbufs; ++i) {
         segs += (lens[i] + seg - 1) / seg;
-        segs_skip += (lens[i] + seg_skip - 1) / seg_skip;
         tasks += (lens[i] + task_bytes - 1) / task_bytes;
     }
-    if (segs >= 0xFFFF0000ull || segs_skip >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
+    if (segs >= 0xFFFF0000ull || tasks >= 0xFFFF0000ull) return CDC_E_INVALID;
     plan->total_segs = uint32_t(segs);
-    plan->total_segs_skip = uint32_t(segs_skip);
     plan->total_tasks = uint32_t(tasks);
-    if (segs_skip > segs) segs = segs_skip;  // the per-segment arrays serve either mode
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -2489,7 +2235,8 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_xg = take(segs * 8);
     plan->off_sg = take(segs * 8);
     plan->off_flags = take(kMaxBufsPerLaunch * 4);
-    plan->off_tick = take(4 * 4);  // [0] k_resolve / k_walk ticket, [2] persistent scan task counter
+    plan->off_tick = take(8 * 4);  // [0] segment ticket, [2] persistent scan task counter, [3..5] k_chunk tiers
+    plan->off_tdone = take(tasks * 4);
     plan->off_runsL = take(tasks * 64 * 8);
     plan->off_validL = take(tasks * 4);
     plan->bytes = off;
@@ -2529,23 +2276,28 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     for (uint32_t i = 0; i < B.nbufs; ++i) bytes += B.b[i].len;
     ProfRec pr;
     const bool prof = prof_begin(pr, bytes);
-    if (B.skip) {  // the skip walk: granules zeroed, then one kernel
-        const size_t zb = size_t(reinterpret_cast<char *>(W.tick + 2) - reinterpret_cast<char *>(W.xg));
+    // With profiling on, the events ride on the kernels' own dispatch packets
+    // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
+    const uint32_t need_wgs = (B.total_tasks + kS2Waves - 1) / kS2Waves;
+    if (B.one_launch) {  // k_chunk: counters, flags and granules zeroed, then one kernel
+        const size_t zb = size_t(reinterpret_cast<char *>(W.tdone + B.total_tasks) - reinterpret_cast<char *>(W.xg));
         if (hipMemsetAsync(W.xg, 0, zb, st) != hipSuccess) return CDC_E_DEVICE;
-        const dim3 rgrid(B.total_segs > 0 ? (B.total_segs + kWalkWavesPerWG - 1) / kWalkWavesPerWG : 1u);
+        uint32_t wgs = need_wgs > 0 ? need_wgs : 1u;
+        if (B.persist && B.scan_wgs < wgs) wgs = B.scan_wgs;
         if (prof) {
-            hipExtLaunchKernelGGL(k_walk, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
+            hipExtLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
             std::lock_guard<std::mutex> lk(g_prof_mu);
             (void)hipEventRecord(pr.e2, st);
             g_prof_live.push_back(pr);
         } else {
-            hipLaunchKernelGGL(k_walk, rgrid, dim3(kWalkWavesPerWG * 64), 0, st, B, P, W);
+            hipLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, B, P, W);
         }
+        // the adaptive MaskL probe reads this launch's records; it only sets the hint for later groups
+        if (B.total_tasks > 0 && B.maskl_probe)
+            hipLaunchKernelGGL(k_maskl_probe, dim3((B.total_tasks + kProbeWaves - 1) / kProbeWaves),
+                               dim3(kProbeWaves * 64), 0, st, B, P, W);
         return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
     }
-    // With profiling on, the events ride on the kernels' own dispatch packets
-    // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
-    const uint32_t need_wgs = (B.total_tasks + kS2Waves - 1) / kS2Waves;
     const dim3 sgrid(B.persist && B.scan_wgs < need_wgs ? B.scan_wgs : need_wgs), sblock(kS2Waves * 64);
     const bool fused = B.maskl_index && B.maskl_fused;  // k_scan_f: both indexes in one pass
     if (B.persist && B.total_tasks > 0 && hipMemsetAsync(W.tick + 2, 0, 4, st) != hipSuccess) return CDC_E_DEVICE;

@@ -95,6 +95,13 @@ def set_maskl_index_mode(mode):
     check(lib().cdc_set_maskl_index_mode(int(mode)))
 
 
+def set_resolve_mode(mode):
+    """1 = the scan and the chain resolution in one launch (k_chunk, the
+    default wherever a launch group needs no MaskL index), 0 = always two
+    launches (k_scan + k_resolve). Cut points do not depend on it."""
+    check(lib().cdc_set_resolve_mode(int(mode)))
+
+
 def maskl_state(device=0):
     """Adaptive MaskL state (diagnostics): (1 while the next launch groups
     build the MaskL index because a recent group asked for MaskL candidates,

@@ -67,7 +67,9 @@ class ChunkRecords(collections.abc.Sequence):
     when it is read (Distribution = histogram / length, as chunkify_batch
     computes it).  A backup reports tens of thousands of chunks per run; as
     arrays they cost the callbacks a few copies instead of an object each
-    (and the cyclic collector nothing)."""
+    (and the cyclic collector nothing).  Read-only: indexing makes a new
+    Chunk each time, so edits to it are not kept (to_list() gives a list of
+    Chunks to edit); == compares chunk by chunk with any sequence of Chunks."""
     __slots__ = ("_dg", "_lens", "_ent", "_hist")
 
     def __init__(self, dg=b"", lens=None, ent=None, hist=None):
@@ -100,6 +102,20 @@ class ChunkRecords(collections.abc.Sequence):
         length = int(self._lens[k])
         return hashing.Chunk(self._dg[32 * k:32 * k + 32], length, float(self._ent[k]),
                              self._hist[k] / float(max(length, 1)))
+
+    def to_list(self):
+        """The chunks as a list of hashing.Chunk (copies)."""
+        return [self[i] for i in range(len(self))]
+
+    def __eq__(self, other):
+        if not isinstance(other, collections.abc.Sequence) or isinstance(other, (str, bytes)):
+            return NotImplemented
+        if len(other) != len(self):
+            return False
+        return all(a.Checksum == b.Checksum and a.Length == b.Length and a.Entropy == b.Entropy and
+                   np.array_equal(a.Distribution, b.Distribution) for a, b in zip(self, other))
+
+    __hash__ = None
 
     def __repr__(self):
         return f"ChunkRecords({len(self)} chunks)"
@@ -342,6 +358,11 @@ class BackupSession:
         errors = []
 
         def on_file(_ctx, fp):
+            # The callback creates a few objects per file; no cyclic
+            # collection (none of them forms a cycle) runs over the whole
+            # heap meanwhile.  Only this thread's callback is covered.
+            gc_was = gc.isenabled()
+            gc.disable()
             try:
                 f = fp.contents
                 i = int(f.index)
@@ -369,6 +390,9 @@ class BackupSession:
                                     ContentType=ctypes_of.pop(i, ""), Entropy=float(f.object_entropy))
             except Exception as e:  # noqa: BLE001 - re-raised after the call
                 errors.append(e)
+            finally:
+                if gc_was:
+                    gc.enable()
 
         def on_pack(_ctx, data, length):
             packs.append(ctypes.string_at(data, length) if keep_packfiles else None)
@@ -376,15 +400,7 @@ class BackupSession:
 
         fcb, pcb = _lib.BACKUP_FILE_FN(on_file), _lib.BACKUP_PACK_FN(on_pack)
         st = _lib.cdc_backup_stats()
-        # The callbacks create an object per chunk; no cyclic collection
-        # (none of them forms a cycle) runs over the whole heap meanwhile.
-        gc_was = gc.isenabled()
-        gc.disable()
-        try:
-            rc = _lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st))
-        finally:
-            if gc_was:
-                gc.enable()
+        rc = _lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st))
         _lib.check(rc, "cdc_backup_files")
         if errors:
             raise errors[0]

@@ -158,6 +158,34 @@ def test_backup_files_larger_than_the_batch_go_in_pieces(tmp_path):
     assert set(_blobs_of(packs, KEY, True)) == {c.Checksum for o in objs for c in o.Chunks}
 
 
+def test_backup_large_file_failing_in_a_middle_piece(tmp_path, monkeypatch):
+    """A file in pieces whose third piece cannot be read (the library's test
+    hook CDC_BACKUP_FAIL_PIECE=file:piece, as a file that shrank mid-run):
+    that file fails (status CDC_E_IO, no object), failed_files is 1, and the
+    other files -- a large one read in pieces beside it included -- are backed
+    up intact.  The failing file's later pieces are read ahead of its device
+    work (piece reads no longer wait for the previous piece's cut list)."""
+    files = [random_bytes(70 << 20, 51).tobytes(), random_bytes(1 << 20, 52).tobytes(),
+             random_bytes(40 << 20, 53).tobytes()]
+    paths = []
+    for i, b in enumerate(files):
+        p = tmp_path / f"m{i}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    monkeypatch.setenv("CDC_BACKUP_FAIL_PIECE", "0:2")
+    with snapshot.BackupSession(key=KEY, batch_bytes=8 << 20, packers=2) as s:
+        objs, packs, st = s.run(paths)
+        failed = dict(s.failed)
+    assert failed == {0: _lib.CDC_E_IO} and objs[0] is None
+    assert st["failed_files"] == 1 and st["files"] == len(files)
+    ref_objs = snapshot.chunkify_batch(files[1:])
+    for o, r, b in zip(objs[1:], ref_objs, files[1:]):
+        assert o.Checksum == r.Checksum == hashlib.sha256(b).digest()
+        assert [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks]
+    stored = set(_blobs_of(packs, KEY, True))
+    assert {c.Checksum for o in objs[1:] for c in o.Chunks} <= stored
+
+
 def test_backup_stats_report_the_hardware_queues():
     """cdc_backup_new records GPU_MAX_HW_QUEUES (0: unset, HIP's default of 4)
     and whether the pipeline's streams share hardware queues."""

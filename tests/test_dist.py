@@ -102,6 +102,25 @@ def test_bench_parity_is_the_and_over_ranks():
     assert line["parity_vs_oracle"] is False
 
 
+@pytest.mark.parametrize("box", ["cpu", pytest.param("gpu-box", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("when", ["before", "after"])
+def test_bench_fails_fast_when_a_rank_dies(box, when):
+    """a failure surfaces as an error, never a hang.  Rank 1
+    exits 3 before the rendezvous (rank 0 would wait in init_process_group) or
+    after it (rank 0 would wait in the next collective): `--gpus 2` returns 3
+    within 60 s, the other rank terminated.  Also run in the GPU suite (the
+    plumbing is the same on the box)."""
+    import time
+    t0 = time.time()
+    rc, line, err = _run_bench(["--gpus", "2"], {"BENCH_CPU_SELFTEST": "1", "BENCH_SELFTEST_FAIL_RANK": "1",
+                                                 "BENCH_SELFTEST_FAIL_AT": when, "BENCH_DIST_TIMEOUT_S": "300"})
+    el = time.time() - t0
+    assert rc == 3, err[-2000:]
+    assert el < 60, f"took {el:.1f} s"
+    assert "rank 1 exited with status 3" in err
+    assert line is None
+
+
 def test_bench_refuses_a_mismatched_launcher():
     """A launcher that started a different number of ranks than --gpus asks
     for is an error, never a silent 1-rank run."""

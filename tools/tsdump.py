@@ -55,11 +55,8 @@ def main():
     scan = ts[K_SCAN:K_RES].reshape(-1, 4)
     scan = scan[scan[:, 0] > 0]
     r0 = ts[K_RES:K_RES + 8 * 16384].reshape(-1, 8)
-    walk = len(scan) == 0  # CDC_WALK_MODE=2: k_walk only
-    t0 = scan[:, 0].min() if not walk else r0[r0[:, 0] > 0, 0].min()
+    t0 = scan[:, 0].min()
     us = lambda x: (x - t0) / 100.0  # 100 MHz
-    if walk:
-        return walk_report(ts, us)
     print(f"scan WGs {len(scan)}: start {pct(us(scan[:, 0]))}")
     print(f"  fill done {pct(us(scan[:, 1]))}")
     print(f"  wave0 end {pct(us(scan[:, 2]))}")
@@ -114,22 +111,6 @@ def main():
     lbs = np.argsort(r[:, 3])[-4:]
     print("  latest look-backs (segment: done at us): " + ", ".join(f"{i}: {us(r[i, 3]):.1f}" for i in lbs))
     print(f"  listed nodes {pct(r[:, 5])}   exact next_node() calls {pct(r[:, 6])}   junction nodes {pct(r[:, 7])}")
-
-
-def walk_report(ts, us):
-    """k_walk (skip walk): per-segment phases; slot 5 holds the wave's skip_scan blocks."""
-    r = ts[K_RES:K_RES + 8 * 16384].reshape(-1, 8)
-    nseg = int(np.count_nonzero(r[:, 4]))
-    r = r[:nseg]
-    print(f"k_walk segs {nseg}: start {pct(us(r[:, 0]))}")
-    print(f"  spec exit published {pct(us(r[:, 2]))}   (- start) {pct((r[:, 2] - r[:, 0]) / 100.0)}")
-    lb = r[1:, 3]
-    print(f"  look-back done {pct(us(lb))}   (- spec) {pct((lb - r[1:, 2]) / 100.0)}")
-    print(f"  inclusive published {pct(us(r[:, 4]))}   per wave (end - start) {pct((r[:, 4] - r[:, 0]) / 100.0)}")
-    print(f"  blocks per wave {pct(r[:, 5])}  total {int(r[:, 5].sum())} (x 16 KiB = {r[:, 5].sum() * 16 / 1024:.0f} MiB)")
-    print(f"  steps per wave {pct(r[:, 6])}   junction nodes {pct(r[:, 7])}")
-    us_per_block = (r[:, 4] - r[:, 0]) / 100.0 / np.maximum(r[:, 5], 1)
-    print(f"  us per block (wave time / blocks) {pct(us_per_block)}")
 
 
 if __name__ == "__main__":
