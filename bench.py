@@ -173,6 +173,23 @@ def digest_leg(torch, batch, bufs, reps, check):
              longest_chunk=longest, kernel="k_chunk_digest (SHA-256: per chunk a producer lane and a round lane) + k_chunk_hist (a wave per chunk)",
              bound="one launch lasts as long as its longest chunk's SHA-256 chain: 64-B blocks x ~905 VALU of one "
                    "round wave per block")
+    # the hybrid single pass (cdc_chunk_digests_hybrid): the longest chunks'
+    # SHA-256 on 16 host cores (the box's CPU share), the rest on the device
+    if len(bufs) <= 32:
+        hout, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res_rows, host_threads=16)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            hout, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res_rows, host_threads=16)
+        torch.cuda.synchronize()
+        hms = (time.perf_counter() - t0) / reps * 1e3
+        same = all(torch.equal(a[0][:c.shape[0]], b[0][:c.shape[0]]) and torch.equal(a[1][:c.shape[0]], b[1][:c.shape[0]])
+                   for a, b, c in zip(out, hout, cuts))
+        d["hybrid"] = dict(value=round(total / (hms * 1e-3) / GIB, 2), unit="GiB/s", ms_per_pass=round(hms, 3),
+                           host_threads=16, host_chunks=hc, host_bytes=hb, equal_to_device_only=bool(same),
+                           note="cdc_chunk_digests_hybrid, wall time incl. the cut lists back to the host: the "
+                                "longest chunks' SHA-256 on host cores (x86 SHA extensions, ~35 ns per 64-B block "
+                                "against a device chain's ~2 us), the rest and every histogram on the device")
     if check:
         host = bufs[0][:min(bufs[0].numel(), 256 << 20)].cpu().numpy()
         c0 = cuts[0].cpu().numpy()

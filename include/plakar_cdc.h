@@ -395,6 +395,23 @@ int cdc_chunk_digests_device_batch_async(int device, const void *const *d_data, 
                                          const cdc_cut *const *d_cuts, const uint64_t *cut_caps,
                                          const cdc_result *const *d_results, uint8_t *const *d_digests,
                                          uint32_t *const *d_hist, void *stream);
+/* Hybrid form, synchronous: as the batched form, except that the longest
+ * chunks' SHA-256 runs on `host_threads` host cores (x86 SHA extensions) while
+ * the device hashes the others and computes every histogram.  A device
+ * SHA-256 chain costs ~2 us per 64-B block against ~35 ns on a host core, and
+ * a device launch lasts as long as its longest chunk, so a single pass over
+ * long chunks ends sooner this way.  host_min_len = 0 picks the host's share
+ * from the lengths (the longest chunks, as many as balance the host's bytes
+ * over its cores and PCIe against the device's longest remaining chain);
+ * otherwise every chunk of at least host_min_len bytes goes to the host.
+ * host_threads = 0: all on the device.  Drains `stream` first (the cut lists
+ * must be final) and returns once every digest and histogram is in device
+ * memory; *host_chunks / *host_bytes (may be NULL) report the host's share.
+ * At most 32 buffers. */
+int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64_t *lens, int nbufs,
+                             const cdc_cut *const *d_cuts, const uint64_t *cut_caps, const cdc_result *const *d_results,
+                             uint8_t *const *d_digests, uint32_t *const *d_hist, int host_threads,
+                             uint64_t host_min_len, void *stream, uint64_t *host_chunks, uint64_t *host_bytes);
 /* entropy() of snapshot/backup.go:548-569 for `rows` histogram rows (256
  * uint32 each, as cdc_chunk_digests* writes them; a row's sum is its chunk's
  * length) into d_entropy (float64 per row): the reference's terms with Go's

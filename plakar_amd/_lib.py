@@ -131,6 +131,11 @@ SIGNATURES = {
                                                             _P(ctypes.c_void_p), _P(ctypes.c_uint64),
                                                             _P(ctypes.c_void_p), _P(ctypes.c_void_p),
                                                             _P(ctypes.c_void_p), ctypes.c_void_p]),
+    "cdc_chunk_digests_hybrid": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_void_p), _P(ctypes.c_uint64), ctypes.c_int,
+                                                _P(ctypes.c_void_p), _P(ctypes.c_uint64), _P(ctypes.c_void_p),
+                                                _P(ctypes.c_void_p), _P(ctypes.c_void_p), ctypes.c_int,
+                                                ctypes.c_uint64, ctypes.c_void_p, _P(ctypes.c_uint64),
+                                                _P(ctypes.c_uint64)]),
     "cdc_batch_new": (ctypes.c_int, [ctypes.c_uint64, _P(ctypes.c_void_p)]),
     "cdc_batch_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, _P(_P(ctypes.c_uint8))]),
     "cdc_batch_add_fd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64]),

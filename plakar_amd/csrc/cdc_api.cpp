@@ -319,7 +319,8 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         B.maskl_hint = ctx->hint_d;
     }
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
-    B.one_launch = resolve_mode().load(std::memory_order_relaxed) == 1 && !B.maskl_index ? 1u : 0u;
+    // one launch (k_chunk / k_chunk_f) unless the MaskL index needs k_scan_l
+    B.one_launch = resolve_mode().load(std::memory_order_relaxed) == 1 && (!B.maskl_index || B.maskl_fused) ? 1u : 0u;
     uint32_t segs = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
         BufDesc &D = B.b[i];
@@ -1081,6 +1082,278 @@ int cdc_chunk_digests_device_async(int device, const void *d_data, uint64_t len,
 {
     return cdc_chunk_digests_device_batch_async(device, &d_data, &len, 1, &d_cuts, &cut_cap, &d_result, &d_digests,
                                                 d_hist ? &d_hist : nullptr, stream);
+}
+
+// ---- hybrid digests: the longest chunks' SHA-256 on host cores -------------
+// One device chain costs ~2.05 us per 64-B block (cdc_digest.hip), a host
+// core with the SHA extensions ~35 ns, so the device's launch, which lasts as
+// long as its longest chunk, ends sooner when the longest chunks go to the
+// host.  Per device, one call at a time; scratch grown on demand and kept.
+}  // extern "C"
+namespace {
+struct HybridScratch {
+    std::mutex mu;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_dig = nullptr;
+    hipEvent_t ev_part[4] = {};
+    // device / pinned host buffers and their capacities in bytes
+    void *d_cuts = nullptr, *d_stage = nullptr, *d_gj = nullptr, *d_sj = nullptr, *d_dig = nullptr;
+    void *h_stage = nullptr, *h_gj = nullptr, *h_sj = nullptr, *h_dig = nullptr;
+    uint64_t c_cuts = 0, c_stage = 0, c_gj = 0, c_sj = 0, c_dig = 0;
+    uint64_t hc_stage = 0, hc_gj = 0, hc_sj = 0, hc_dig = 0;
+};
+
+HybridScratch &hybrid_scratch(int device)
+{
+    static HybridScratch h[64];
+    return h[device & 63];
+}
+
+bool hy_dev(void *&p, uint64_t &cap, uint64_t need)
+{
+    if (need <= cap && p) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const uint64_t n = need + need / 4 + 256;
+    if (hipMalloc(&p, n) != hipSuccess) return false;
+    cap = n;
+    return true;
+}
+
+bool hy_host(void *&p, uint64_t &cap, uint64_t need)
+{
+    if (need <= cap && p) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const uint64_t n = need + need / 4 + 256;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return false;
+    cap = n;
+    return true;
+}
+
+// The host's share: the longest chunks, as many as balance the two sides.
+// Device: the longest chunk left to it (its chain); host: the bytes given to
+// `threads` cores (the longest one's chain at least) plus the copy over PCIe.
+size_t hybrid_split(const std::vector<uint64_t> &sorted_desc, int threads)
+{
+    constexpr double kDevPerByte = 2.05e-6 / 64.0, kHostRate = 1.6e9, kPcie = 40e9;
+    double best = 1e30, bytes = 0;
+    size_t k_best = 0;
+    const size_t n = std::min<size_t>(sorted_desc.size(), 1u << 16);
+    for (size_t k = 0; k <= n; ++k) {
+        const double dev = k < sorted_desc.size() ? double(sorted_desc[k]) * kDevPerByte : 0.0;
+        const double host = k ? std::max(double(sorted_desc[0]) / kHostRate, bytes / (threads * kHostRate)) +
+                                    bytes / kPcie
+                              : 0.0;
+        const double t = std::max(dev, host);
+        if (t < best) {
+            best = t;
+            k_best = k;
+        }
+        if (k < n) bytes += double(sorted_desc[k]);
+    }
+    return k_best;
+}
+}  // namespace
+extern "C" {
+
+int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64_t *lens, int nbufs,
+                             const cdc_cut *const *d_cuts, const uint64_t *cut_caps, const cdc_result *const *d_results,
+                             uint8_t *const *d_digests, uint32_t *const *d_hist, int host_threads,
+                             uint64_t host_min_len, void *stream, uint64_t *host_chunks, uint64_t *host_bytes)
+{
+    if (host_chunks) *host_chunks = 0;
+    if (host_bytes) *host_bytes = 0;
+    if (nbufs < 0 || (nbufs > 0 && (!d_data || !lens || !d_cuts || !cut_caps || !d_digests)) || host_threads < 0 ||
+        host_threads > 256)
+        return CDC_E_INVALID;
+    bool want_hist = false;
+    for (int i = 0; i < nbufs && d_hist; ++i) want_hist |= cut_caps[i] && d_hist[i];
+    for (int i = 0; i < nbufs; ++i) {
+        if ((lens[i] && !d_data[i]) || (cut_caps[i] && (!d_cuts[i] || !d_digests[i]))) return CDC_E_INVALID;
+        if (want_hist && cut_caps[i] && !d_hist[i]) return CDC_E_INVALID;
+    }
+    DeviceCtx *ctx = nullptr;
+    int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    if (host_threads == 0 || nbufs == 0 || nbufs > kMaxBufsPerLaunch)  // all on the device
+        return cdc_chunk_digests_device_batch_async(device, d_data, lens, nbufs, d_cuts, cut_caps, d_results,
+                                                    d_digests, d_hist, stream);
+    if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
+    HybridScratch &H = hybrid_scratch(device);
+    std::lock_guard<std::mutex> lk(H.mu);
+    if (!H.side) {
+        if (hipStreamCreateWithFlags(&H.side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&H.ev_dig, hipEventDisableTiming) != hipSuccess)
+            return CDC_E_DEVICE;
+        for (auto &e : H.ev_part)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return CDC_E_DEVICE;
+    }
+    // the cut lists, final once the caller's stream is drained
+    if (hipStreamSynchronize(sm) != hipSuccess) return CDC_E_DEVICE;
+    std::vector<uint64_t> cnt(static_cast<size_t>(nbufs)), base(static_cast<size_t>(nbufs) + 1, 0);
+    for (int i = 0; i < nbufs; ++i) {
+        uint64_t c = cut_caps[i];
+        if (d_results && d_results[i] && c) {
+            cdc_result r;
+            if (hipMemcpy(&r, d_results[i], sizeof(r), hipMemcpyDeviceToHost) != hipSuccess) return CDC_E_DEVICE;
+            c = std::min<uint64_t>(c, r.ncuts);
+        }
+        cnt[size_t(i)] = c;
+        base[size_t(i) + 1] = base[size_t(i)] + c;
+    }
+    const uint64_t total = base[size_t(nbufs)];
+    std::vector<cdc_cut> cuts(total);
+    for (int i = 0; i < nbufs; ++i)
+        if (cnt[size_t(i)] && hipMemcpy(cuts.data() + base[size_t(i)], d_cuts[i], cnt[size_t(i)] * sizeof(cdc_cut),
+                                        hipMemcpyDeviceToHost) != hipSuccess)
+            return CDC_E_DEVICE;
+    // chunk lengths as the kernels see them (clipped to the buffer), buffer of each row
+    std::vector<uint64_t> L(total);
+    std::vector<int> bof(total);
+    for (int i = 0; i < nbufs; ++i)
+        for (uint64_t q = base[size_t(i)]; q < base[size_t(i) + 1]; ++q) {
+            const cdc_cut &c = cuts[q];
+            L[q] = c.offset >= lens[i] ? 0ull : std::min<uint64_t>(c.length, lens[i] - c.offset);
+            bof[q] = i;
+        }
+    std::vector<uint64_t> order(total);
+    for (uint64_t q = 0; q < total; ++q) order[q] = q;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return L[a] > L[b]; });
+    size_t k = 0;
+    if (host_min_len) {
+        while (k < total && L[order[k]] >= host_min_len) ++k;
+    } else {
+        std::vector<uint64_t> sd(total);
+        for (uint64_t q = 0; q < total; ++q) sd[q] = L[order[q]];
+        k = hybrid_split(sd, host_threads);
+    }
+    while (k > 0 && L[order[k - 1]] == 0) --k;  // empty chunks stay on the device
+    if (k == 0)
+        return cdc_chunk_digests_device_batch_async(device, d_data, lens, nbufs, d_cuts, cut_caps, d_results,
+                                                    d_digests, d_hist, stream);
+    // the device's lists: the host's chunks as empty ones (their rows are overwritten below)
+    std::vector<cdc_cut> mod(cuts);
+    uint64_t hbytes = 0;
+    std::vector<uint64_t> soff(k);  // staging offset of host chunk j (16-B aligned)
+    for (size_t j = 0; j < k; ++j) {
+        mod[order[j]].length = 0;
+        soff[j] = hbytes;
+        hbytes += (L[order[j]] + 15) & ~15ull;
+    }
+    if (!hy_dev(H.d_cuts, H.c_cuts, total * sizeof(cdc_cut)) || !hy_dev(H.d_stage, H.c_stage, hbytes + 64) ||
+        !hy_host(H.h_stage, H.hc_stage, hbytes + 64) || !hy_dev(H.d_gj, H.c_gj, k * sizeof(GatherJob)) ||
+        !hy_host(H.h_gj, H.hc_gj, k * sizeof(GatherJob)) || !hy_dev(H.d_sj, H.c_sj, k * sizeof(ScatterJob)) ||
+        !hy_host(H.h_sj, H.hc_sj, k * sizeof(ScatterJob)) || !hy_dev(H.d_dig, H.c_dig, 32 * k) ||
+        !hy_host(H.h_dig, H.hc_dig, 32 * k))
+        return CDC_E_DEVICE;
+    cdc_cut *dcuts = static_cast<cdc_cut *>(H.d_cuts);
+    uint8_t *dstage = static_cast<uint8_t *>(H.d_stage), *hstage = static_cast<uint8_t *>(H.h_stage);
+    GatherJob *hgj = static_cast<GatherJob *>(H.h_gj), *dgj = static_cast<GatherJob *>(H.d_gj);
+    ScatterJob *hsj = static_cast<ScatterJob *>(H.h_sj), *dsj = static_cast<ScatterJob *>(H.d_sj);
+    uint8_t *hdig = static_cast<uint8_t *>(H.h_dig), *ddig = static_cast<uint8_t *>(H.d_dig);
+    // the copy from pageable memory completes before hipMemcpyAsync returns
+    if (hipMemcpyAsync(dcuts, mod.data(), total * sizeof(cdc_cut), hipMemcpyHostToDevice, sm) != hipSuccess)
+        return CDC_E_DEVICE;
+    // device: SHA-256 of every other chunk (the modified lists), histograms of all (the caller's lists)
+    {
+        DigestBatch DB;
+        std::memset(&DB, 0, sizeof(DB));
+        DB.nbufs = uint32_t(nbufs);
+        for (int i = 0; i < nbufs; ++i)
+            DB.b[i] = DigestBuf{static_cast<const uint8_t *>(d_data[i]), lens[i], dcuts + base[size_t(i)],
+                                cnt[size_t(i)], nullptr, d_digests[i], nullptr};
+        if ((st = launch_digests(DB, sm, 1)) != CDC_OK) return st;
+        if (want_hist) {
+            for (int i = 0; i < nbufs; ++i)
+                DB.b[i] = DigestBuf{static_cast<const uint8_t *>(d_data[i]), lens[i], d_cuts[i], cnt[size_t(i)],
+                                    nullptr, d_digests[i], cnt[size_t(i)] ? d_hist[i] : nullptr};
+            if ((st = launch_digests(DB, sm, 2)) != CDC_OK) return st;
+        }
+        if (hipEventRecord(H.ev_dig, sm) != hipSuccess) return CDC_E_DEVICE;
+    }
+    // host: the chunks packed on the side stream and copied back in up to
+    // four parts (longest first), each hashed as it lands
+    for (size_t j = 0; j < k; ++j) {
+        const uint64_t q = order[j];
+        const int i = bof[q];
+        hgj[j] = GatherJob{static_cast<const uint8_t *>(d_data[i]) + cuts[q].offset, L[q], soff[j]};
+        hsj[j] = ScatterJob{d_digests[i] + 32 * (q - base[size_t(i)]), ddig + 32 * j};
+    }
+    if (hipMemcpyAsync(dgj, hgj, k * sizeof(GatherJob), hipMemcpyHostToDevice, H.side) != hipSuccess)
+        return CDC_E_DEVICE;
+    const size_t nparts = std::min<size_t>(4, k);
+    std::vector<size_t> pend(nparts + 1, 0);  // part p: jobs [pend[p], pend[p + 1]), about equal bytes
+    for (size_t p = 1; p < nparts; ++p) {
+        const uint64_t want = hbytes * p / nparts;
+        size_t j = pend[p - 1] + 1;
+        while (j < k && soff[j] < want) ++j;
+        pend[p] = std::min(j, k);
+    }
+    pend[nparts] = k;
+    for (size_t p = 0; p < nparts; ++p) {
+        const size_t j0 = pend[p], j1 = pend[p + 1];
+        if (j1 > j0) {
+            const uint64_t b0 = soff[j0], b1 = j1 < k ? soff[j1] : hbytes;
+            if ((st = launch_gather(dgj + j0, uint32_t(j1 - j0), dstage, H.side)) != CDC_OK) return st;
+            if (hipMemcpyAsync(hstage + b0, dstage + b0, b1 - b0, hipMemcpyDeviceToHost, H.side) != hipSuccess)
+                return CDC_E_DEVICE;
+        }
+        if (hipEventRecord(H.ev_part[p], H.side) != hipSuccess) return CDC_E_DEVICE;
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<int> fail{CDC_OK};
+    std::vector<std::atomic<int>> landed(nparts);
+    for (auto &x : landed) x.store(0);
+    std::mutex pmu;
+    auto worker = [&]() {
+        for (;;) {
+            const size_t j = next.fetch_add(1);
+            if (j >= k || fail.load() != CDC_OK) return;
+            size_t p = 0;
+            while (p + 1 < nparts && j >= pend[p + 1]) ++p;
+            if (!landed[p].load(std::memory_order_acquire)) {
+                std::lock_guard<std::mutex> g(pmu);
+                if (!landed[p].load()) {
+                    if (hipEventSynchronize(H.ev_part[p]) != hipSuccess) {
+                        fail.store(CDC_E_DEVICE);
+                        return;
+                    }
+                    landed[p].store(1, std::memory_order_release);
+                }
+            }
+            sha256(hstage + soff[j], size_t(L[order[j]]), hdig + 32 * j);
+        }
+    };
+    std::vector<std::thread> ts;
+    try {
+        for (int t = 1; t < host_threads; ++t) ts.emplace_back(worker);
+    } catch (...) {
+        fail.store(CDC_E_NOMEM);
+    }
+    worker();
+    for (auto &t : ts) t.join();
+    if (fail.load() != CDC_OK) {
+        (void)hipStreamSynchronize(H.side);
+        return fail.load();
+    }
+    // the host's digests into their rows, after the device's digest kernel
+    if (hipStreamWaitEvent(H.side, H.ev_dig, 0) != hipSuccess ||
+        hipMemcpyAsync(ddig, hdig, 32 * k, hipMemcpyHostToDevice, H.side) != hipSuccess ||
+        hipMemcpyAsync(dsj, hsj, k * sizeof(ScatterJob), hipMemcpyHostToDevice, H.side) != hipSuccess)
+        return CDC_E_DEVICE;
+    if ((st = launch_scatter_digests(dsj, uint32_t(k), H.side)) != CDC_OK) return st;
+    if (hipStreamSynchronize(H.side) != hipSuccess || hipStreamSynchronize(sm) != hipSuccess) return CDC_E_DEVICE;
+    if (host_chunks) *host_chunks = k;
+    if (host_bytes) {
+        uint64_t b = 0;
+        for (size_t j = 0; j < k; ++j) b += L[order[j]];
+        *host_bytes = b;
+    }
+    return CDC_OK;
 }
 
 int cdc_chunk_entropy_device_async(int device, const uint32_t *d_hist, uint64_t rows, double *d_entropy, void *stream)

@@ -614,15 +614,16 @@ uint32_t device_cus()
 }
 
 template <bool kInd>
-int launch_digest_kernels(DigestBatch D, uint64_t cap, bool hist, hipStream_t st)
+int launch_digest_kernels(DigestBatch D, uint64_t cap, bool hist, hipStream_t st, int parts = 3)
 {
     static const uint32_t cus = device_cus();
     // two SHA-256 workgroups per CU (~66 KiB of LDS each)
     D.resident_lanes = g_digest_lanes ? g_digest_lanes : uint64_t(cus) * 2u * 64u * kDigestGroups;
     const uint32_t lanes_per_wg = 64u * kDigestGroups;
-    hipLaunchKernelGGL(k_chunk_digest<kInd>, dim3(uint32_t((cap + lanes_per_wg - 1) / lanes_per_wg), D.nbufs),
-                       dim3(kDigestWaves * 64), 0, st, D);
-    if (hist) {  // a wave per chunk; up to 8 workgroups per CU
+    if (parts & 1)
+        hipLaunchKernelGGL(k_chunk_digest<kInd>, dim3(uint32_t((cap + lanes_per_wg - 1) / lanes_per_wg), D.nbufs),
+                           dim3(kDigestWaves * 64), 0, st, D);
+    if (hist && (parts & 2)) {  // a wave per chunk; up to 8 workgroups per CU
         const uint64_t wgs = std::min<uint64_t>((cap + kHistWaves - 1) / kHistWaves, uint64_t(cus) * 8u);
         hipLaunchKernelGGL(k_chunk_hist<kInd>, dim3(uint32_t(wgs), D.nbufs), dim3(kHistWaves * 64), 0, st, D);
     }
@@ -649,7 +650,7 @@ DescRing &desc_ring(int device)
 
 }  // namespace
 
-int launch_digests(const DigestBatch &DB, void *stream)
+int launch_digests(const DigestBatch &DB, void *stream, int parts)
 {
     uint64_t cap = 0;
     bool hist = false;
@@ -661,7 +662,56 @@ int launch_digests(const DigestBatch &DB, void *stream)
     if (cap > 0xFFFFFFFFull) return CDC_E_INVALID;  // chunk indices relative to a workgroup's first are u32
     DigestBatch D = DB;
     D.ind = nullptr;
-    return launch_digest_kernels<false>(D, cap, hist, reinterpret_cast<hipStream_t>(stream));
+    return launch_digest_kernels<false>(D, cap, hist, reinterpret_cast<hipStream_t>(stream), parts);
+}
+
+// ---------------------------------------------------------------------------
+// Hybrid digests (cdc_chunk_digests_hybrid): the longest chunks' SHA-256 on
+// host cores.  A chain costs the device ~2 us per 64-B block (one round wave,
+// above) against ~35 ns on a host core with the SHA extensions, so a launch
+// that lasts as long as its longest chunk ends sooner when the longest go to
+// the host.  k_gather packs those chunks' bytes into a staging buffer (one
+// workgroup per chunk, aligned dwords funnel-shifted, reads clamped to the
+// chunk's last dword) for one copy to the host; k_scatter_digests writes the
+// host's digests back into the caller's digest rows.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gather(const GatherJob *jobs, uint8_t *stage)
+{
+    const GatherJob J = jobs[blockIdx.x];
+    if (J.len == 0) return;
+    const uint64_t s = reinterpret_cast<uint64_t>(J.src);
+    const uint32_t sh = uint32_t(s & 3u);
+    const uint32_t *a = reinterpret_cast<const uint32_t *>(s & ~3ull);
+    const uint64_t nd = (J.len + 3) / 4;
+    const uint64_t last = (s + J.len - 1 - (s & ~3ull)) / 4;  // the last dword holding a chunk byte
+    uint32_t *d = reinterpret_cast<uint32_t *>(stage + J.dst);
+    for (uint64_t i = threadIdx.x; i < nd; i += blockDim.x) {
+        const uint32_t lo = a[min(i, last)], hi = a[min(i + 1, last)];
+        d[i] = __builtin_amdgcn_alignbyte(hi, lo, sh);  // bytes sh .. sh + 3 of hi:lo
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scatter_digests(const ScatterJob *jobs, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 8u * n) return;
+    const ScatterJob J = jobs[i / 8u];
+    reinterpret_cast<uint32_t *>(J.dst)[i % 8u] = reinterpret_cast<const uint32_t *>(J.src)[i % 8u];
+}
+
+int launch_gather(const GatherJob *d_jobs, uint32_t n, uint8_t *d_stage, void *stream)
+{
+    if (n == 0) return CDC_OK;
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), d_jobs, d_stage);
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
+}
+
+int launch_scatter_digests(const ScatterJob *d_jobs, uint32_t n, void *stream)
+{
+    if (n == 0) return CDC_OK;
+    hipLaunchKernelGGL(k_scatter_digests, dim3((8u * n + 255u) / 256u), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_jobs, n);
+    return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
 }
 
 int launch_digests_many(const DigestBuf *bufs, uint32_t nbufs, void *stream)

@@ -1364,8 +1364,9 @@ __global__ __launch_bounds__(kGcmWaves * 64) void k_gcm(const Batch B)
     const uint32_t total = B.piece_base[B.nblobs];
     if (B.status[0]) return;
     for (;;) {
-    uint32_t pc = 0;
-    if (lane == 0) pc = atomicAdd(reinterpret_cast<uint32_t *>(&B.status[1]), 1u);
+    // every lane in the atomic (lane 0 adds 1): no lane-0 branch before the
+    // readfirstlane, which the compiler could thread apart (cdc_kernels.hip wave_ticket)
+    uint32_t pc = atomicAdd(reinterpret_cast<uint32_t *>(&B.status[1]), lane == 0 ? 1u : 0u);
     pc = uint32_t(__builtin_amdgcn_readfirstlane(int(pc)));
     if (pc >= total) break;
     uint32_t b;

@@ -85,7 +85,7 @@ struct Workspace {
     uint64_t *w1_nodes;  // [total_segs * 64] speculative chain of each segment
     uint64_t *xg;        // [total_segs] granule: published | node count | speculative exit X_q
     uint64_t *sg;        // [total_segs] granule: LOCAL (conv, cuts) or INCLUSIVE (E, O)
-    uint32_t *flags;     // [kMaxBufsPerLaunch] per-buffer "resolve sequentially"
+    uint32_t *flags;     // [kMaxBufsPerLaunch + 4] per-buffer "resolve sequentially", then the abort word
     uint32_t *tick;      // [8] [0] segment ticket, [2] persistent scan task counter, [3..5] k_chunk tier counters
     // k_chunk: per scan task, 1 once its run records are stored (write-through)
     // and readable by another workgroup.  xg .. tdone is one contiguous range,
@@ -127,7 +127,21 @@ struct DigestBatch {
     const DigestBuf *ind;     // launch_digests_many: the nbufs descriptors in device memory (b unused)
     DigestBuf b[kMaxBufsPerLaunch];
 };
-int launch_digests(const DigestBatch &DB, void *stream);
+// parts: 1 the SHA-256 kernel only, 2 the histograms only, 3 both
+int launch_digests(const DigestBatch &DB, void *stream, int parts = 3);
+// cdc_chunk_digests_hybrid's device pieces: pack chunks into a staging buffer
+// (dst: 16-B aligned offsets), and write 32-B digests to their rows.
+struct GatherJob {
+    const uint8_t *src;
+    uint64_t len;
+    uint64_t dst;
+};
+struct ScatterJob {
+    uint8_t *dst;
+    const uint8_t *src;
+};
+int launch_gather(const GatherJob *d_jobs, uint32_t n, uint8_t *d_stage, void *stream);
+int launch_scatter_digests(const ScatterJob *d_jobs, uint32_t n, void *stream);
 // More than kMaxBufsPerLaunch buffers in ONE launch group: the descriptors go
 // to device memory through a per-device pinned ring (a launch lasts as long as
 // its longest chunk, so several groups of 32 would each pay that tail).

@@ -221,14 +221,51 @@ constexpr uint32_t kTsClk = kTsRes + 8 * 16384;     // clock ring (B.debug & kDb
 constexpr uint32_t kClkRecs = 4096;
 constexpr uint32_t kTsClkN = kTsClk + 4 * kClkRecs;   // ring counter
 constexpr uint32_t kTsHw = kTsClkN + 1;               // per scan workgroup: XCC_ID << 32 | HW_ID (kDbgTs)
-constexpr uint32_t kTsSlots = kTsHw + 4096;
+constexpr uint32_t kTsAbort = kTsHw + 4096;           // the last wait that gave up: kind, two values, time
+constexpr uint32_t kTsTask = kTsAbort + 4;            // k_chunk (kDbgTs): per scan task start, end, wave, XCC << 32 | HW_ID
+constexpr uint32_t kTsTasks = 8192;
+constexpr uint32_t kTsSlots = kTsTask + 4 * kTsTasks;
 constexpr uint32_t kDbgClk = 64;
+constexpr uint32_t kDbgScanOnly = 256;  // k_chunk: waves exit after the scan (no cut lists; timing / hang probes)
 __device__ uint64_t g_ts[kTsSlots];
 
 __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
 {
     if ((B.debug & kDbgTs) && slot < kTsSlots) g_ts[slot] = v == ~0ull ? __builtin_amdgcn_s_memrealtime() : v;
 }
+
+// Bounded waits.  Every spin of a walker (task flags, granules, look-back
+// statuses) gives up after kSpinLimit of its own waiting (s_memrealtime,
+// 100 MHz) or as soon as another wait of the launch gave up: it raises the
+// launch's abort word (W.flags[kAbortWord]), records what it waited for at
+// g_ts[kTsAbort], and the launch's result rows report CDC_E_DEVICE instead
+// of the device hanging.  No correct launch waits that long.
+constexpr uint32_t kAbortWord = kMaxBufsPerLaunch;
+constexpr uint64_t kSpinLimit = 200000000ull;  // 2 s
+enum : uint32_t { kWaitTask = 1, kWaitJunction, kWaitPrev, kWaitLook, kWaitLookSlow, kWaitLast };
+
+struct SpinGuard {
+    uint64_t t0 = 0;
+    // true: poll again; false: give up
+    __device__ __forceinline__ bool ok(uint32_t *flags, uint32_t kind, uint64_t a, uint64_t b)
+    {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (!t0) {
+            t0 = now;
+            return true;
+        }
+        if (__hip_atomic_load(flags + kAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (now - t0 < kSpinLimit) return true;
+        if ((threadIdx.x & 63u) == 0) {
+            __hip_atomic_store(flags + kAbortWord, kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g_ts[kTsAbort] = kind;
+            g_ts[kTsAbort + 1] = a;
+            g_ts[kTsAbort + 2] = b;
+            g_ts[kTsAbort + 3] = now;
+        }
+        return false;
+    }
+};
 
 // ---------------------------------------------------------------------------
 // k_scan: the byte scan.  Each wave owns 64 lane runs of B.scan_lane bytes
@@ -298,6 +335,19 @@ __device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, con
                  : [keep] "=&s"(keep)
                  : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), [base] "s"(base), [dst] "s"(dst)
                  : "memory", "scc");
+}
+
+// One ticket per wave from an agent-scope counter.  Every lane takes part in
+// the atomic (lane 0 adds 1, the others 0), so no lane-0 branch precedes the
+// readfirstlane: after such a branch the compiler may thread it into a
+// neighbouring lane-0 branch (k_chunk's flag store before its next claim),
+// and the readfirstlane then runs for lanes 1-63 while lane 0 is still on the
+// other path -- they read 0 and loop on task 0 (measured: a hang).
+__device__ __forceinline__ uint32_t wave_ticket(uint32_t *p)
+{
+    const uint32_t old = __hip_atomic_fetch_add(p, (threadIdx.x & 63u) == 0u ? 1u : 0u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(old);
 }
 
 __device__ __forceinline__ uint32_t scan_wave_max(uint32_t v)
@@ -484,7 +534,7 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             W.xg[i] = 0ull;
             W.sg[i] = 0ull;
         }
-        if (gt < kMaxBufsPerLaunch) W.flags[gt] = 0u;
+        if (gt < kMaxBufsPerLaunch + 4) W.flags[gt] = 0u;  // + the abort word
         if (gt < 2) W.tick[gt] = 0u;
         if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
     }
@@ -512,11 +562,7 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
     // buffer, and a workgroup that starts late (its CU held by another
     // stream's kernel) finds the tasks taken instead of holding the launch.
     const bool persist = !kMaskL && B.persist != 0;
-    auto next_task = [&]() {
-        uint32_t t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(W.tick + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return uint32_t(__builtin_amdgcn_readfirstlane(t));
-    };
+    auto next_task = [&]() { return wave_ticket(W.tick + 2); };
     for (uint32_t cur = persist ? next_task() : task;;) {
         if (cur >= B.total_tasks) break;
         scan_task<kMaskL, kFused>(B, P, W, s_lds, tab, cur, lane, wave, laneoff);
@@ -918,6 +964,7 @@ struct WalkCtx {
     // before the launch; [dlo, dhi) tasks already seen done (wave-uniform).
     const g_u32 *tdone;
     mutable uint32_t dlo, dhi;
+    uint32_t *flags;  // the launch's flags (the abort word: bounded waits)
 };
 
 // Wait until the scan tasks holding runs [r_lo, r_hi] of the buffer have
@@ -928,9 +975,11 @@ __device__ __forceinline__ void wait_runs(const WalkCtx &C, uint32_t t0, uint32_
 {
     for (uint32_t b0 = t0; b0 <= t1; b0 += 64) {
         const uint32_t t = b0 + C.lane;
+        SpinGuard sp;
         for (;;) {
             const uint32_t v = t <= t1 ? __hip_atomic_load(C.tdone + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
-            if (!__ballot(v == 0u)) break;
+            const uint64_t m = __ballot(v == 0u);
+            if (!m || !sp.ok(C.flags, kWaitTask, b0 + uint32_t(__ffsll((unsigned long long)m) - 1), t1)) break;
             __builtin_amdgcn_s_sleep(2);
         }
     }
@@ -1526,6 +1575,7 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.tdone = B.one_launch ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.tdone + D.task_base)) : nullptr;
     C.dlo = 0;
     C.dhi = 0;
+    C.flags = W.flags;
     return C;
 }
 
@@ -1587,12 +1637,13 @@ __device__ __forceinline__ void drain_stores()
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Poll a granule (every lane the same word) until it is non-zero.
-__device__ __forceinline__ uint64_t wait_granule(const uint64_t *p)
+// Poll a granule (every lane the same word) until it is non-zero (0 if the wait gave up).
+__device__ __forceinline__ uint64_t wait_granule(const uint64_t *p, uint32_t *flags, uint64_t what)
 {
+    SpinGuard sp;
     for (;;) {
         const uint64_t v = readlane64(ld_rlx(p), 0);
-        if (v) return v;
+        if (v || !sp.ok(flags, kWaitPrev, what, 0)) return v;
         __builtin_amdgcn_s_sleep(kSpinSleep);
     }
 }
@@ -1653,12 +1704,14 @@ __device__ __forceinline__ uint32_t row_incl_sum32(uint32_t x)
     return x;
 }
 
-__device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O)
+__device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O,
+                                      uint32_t *flags)
 {
     uint32_t Fe = q + lane;  // F, lane t < kJ: entering at hi + 1 + t leaves E = Fe with Fo cuts added
     uint64_t Fo = 0;
     bool slow = false;
     for (int64_t lo0 = int64_t(q) - 64;; lo0 -= 64 * int64_t(kLbWin)) {
+        if (lo0 + 64 <= 0 && lo0 < int64_t(q) - 64) goto slow_path;  // below segment 0 (never, unless statuses are stale)
         uint64_t sw[kLbWin];
 #pragma unroll
         for (uint32_t w = 0; w < kLbWin; ++w) {
@@ -1671,10 +1724,16 @@ __device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t l
             const int64_t p = lo + int64_t(lane);
             const bool valid = p >= 0;
             uint64_t s = sw[w];
-            if (valid) {
-                while (!s) {
+            {
+                SpinGuard sp;
+                while (__ballot(valid && !s)) {
+                    if (!sp.ok(flags, kWaitLook, q, uint64_t(lo0))) {
+                        E = kSegEnd;  // gave up: the launch reports CDC_E_DEVICE
+                        O = 0;
+                        return;
+                    }
                     __builtin_amdgcn_s_sleep(kSpinSleep);
-                    s = ld_rlx(sg + p);
+                    if (valid && !s) s = ld_rlx(sg + p);
                 }
             }
             const uint64_t im = __ballot(valid && (s >> 62) == 2);
@@ -1747,7 +1806,15 @@ __device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t l
     }
 slow_path:  // q - 1's own INCLUSIVE status
     uint64_t sq;
-    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) != 2) __builtin_amdgcn_s_sleep(kSpinSleep);
+    SpinGuard sp;
+    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) != 2) {
+        if (!sp.ok(flags, kWaitLookSlow, q, 0)) {
+            E = kSegEnd;
+            O = 0;
+            return;
+        }
+        __builtin_amdgcn_s_sleep(kSpinSleep);
+    }
     E = uint32_t((sq >> 38) & 0xFFFFFFu);
     O = sq & ((1ull << 38) - 1);
 }
@@ -1811,7 +1878,9 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 for (;;) {
                     pm |= 1ull << gi;
                     const uint32_t nxt = uint32_t(__builtin_amdgcn_readlane(int(G.si[0]), int(gi)));
-                    if (nxt == kGNone) break;
+                    // successors ascend, so a node seen again means records that
+                    // are not this launch's: stop (the walk below decides)
+                    if (nxt == kGNone || nxt >= 64u || ((pm >> nxt) & 1ull)) break;
                     gi = nxt;
                 }
                 ns = uint32_t(__popcll(pm));
@@ -1835,7 +1904,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 ex = X;
                 break;
             }
-            const uint64_t xp = wait_granule(W.xg + g - 1);  // its load drained this wave's node-list stores
+            const uint64_t xp = wait_granule(W.xg + g - 1, W.flags, g);  // its load drained this wave's node-list stores
             drain_stores();
             if (l0) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
             x = x_dec(xp);
@@ -1856,7 +1925,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                         }
                         pj |= 1ull << gi;
                         const uint32_t nxt = uint32_t(__builtin_amdgcn_readlane(int(G.si[0]), int(gi)));
-                        if (nxt == kGNone) break;
+                        if (nxt == kGNone || nxt >= 64u || ((pj >> nxt) & 1ull)) break;
                         gi = nxt;
                     }
                     c2 = uint32_t(__popcll(pj));
@@ -1897,12 +1966,14 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                             // has taken: phase A never waits for a later one, so
                             // the wait ends; an untaken segment is walked through)
                             uint64_t xr;
+                            SpinGuard sp;
                             for (;;) {
                                 xr = readlane64(ld_rlx(W.xg + base + r), 0);
                                 if (xr & kXNodes) break;
                                 if (kGate &&
                                     __hip_atomic_load(W.tick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= base + r)
                                     break;
+                                if (!sp.ok(W.flags, kWaitJunction, g, base + r)) break;
                                 __builtin_amdgcn_s_sleep(kSpinSleep);
                             }
                             cur = uint32_t(r);
@@ -1978,7 +2049,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     uint64_t O = 0;
     if (q > 0) {
         if (l0) st_rlx(W.sg + g, kKindLocal | (uint64_t(conv == kConvEnd ? kConvEnd : conv - q) << 40) | cuts);
-        lookback(sgb, q, lane, E, O);
+        lookback(sgb, q, lane, E, O, W.flags);
     }
     if (l0) dbg_ts(B, kTsRes + 8 * g + 3);
     const bool on = E == q;
@@ -2017,8 +2088,14 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     if (q + 1 != D.nseg) return;
     // ---- the buffer's last segment: the result row, or the sequential fallback
     if (fb || __hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        for (uint32_t p = lane; p < q; p += 64)
-            while ((ld_rlx(sgb + p) >> 62) != 2) __builtin_amdgcn_s_sleep(kSpinSleep);
+        for (uint32_t p0 = 0; p0 < q; p0 += 64) {
+            const uint32_t p = p0 + lane;
+            SpinGuard sp;
+            while (__ballot(p < q && (ld_rlx(sgb + min(p, q - 1)) >> 62) != 2)) {
+                if (!sp.ok(W.flags, kWaitLast, g, p0)) break;
+                __builtin_amdgcn_s_sleep(kSpinSleep);
+            }
+        }
         if (__hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || fb) {
             resolve_sequential<kGate>(C, P, D);
             return;
@@ -2026,8 +2103,9 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     }
     if (l0) {
         uint64_t *r = reinterpret_cast<uint64_t *>(D.res);
+        const bool ab = __hip_atomic_load(W.flags + kAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         st_rlx(&D.res->ncuts, Oq <= D.cap ? Oq : D.cap);
-        st_rlx(r + 2, uint64_t(int64_t(Oq <= D.cap ? CDC_OK : CDC_E_NOSPACE)));
+        st_rlx(r + 2, uint64_t(int64_t(ab ? CDC_E_DEVICE : Oq <= D.cap ? CDC_OK : CDC_E_NOSPACE)));
         st_rlx(&D.res->needed, Oq);
     }
 }
@@ -2064,7 +2142,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B,
 
 // ---------------------------------------------------------------------------
 // k_chunk: the scan and the chain resolution of a launch group in ONE launch
-// (the launch group needs no MaskL index).  Workgroups as k_scan's (12 waves,
+// (k_chunk_f: with the MaskL index fused into the scan, as k_scan_f).  Workgroups as k_scan's (12 waves,
 // one per CU); every wave first scans, then resolves:
 //
 //   * Scan tasks are claimed, not assigned: the waves of a SIMD finish in age
@@ -2096,11 +2174,16 @@ constexpr uint32_t kTiers = 3;
 static_assert(kS2Waves % kTiers == 0, "tiers of whole SIMD rounds");
 static_assert(kGRecs * 8 <= kStageBytes, "a wave's graph records fit its scan slot");
 
-__global__ __launch_bounds__(kS2Waves * 64) void k_chunk(const Batch B, const DevParams P, const Workspace W)
+template <bool kFused>
+__device__ __forceinline__ void chunk_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
-    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kStageBytes];
-    __shared__ uint64_t s_wtab[256 * kWCopies];
-    __shared__ uint64_t s_gx[kS2Waves][kGExtra];
+    // one array, in a fixed order: the scan's table and slots first, at the
+    // LDS offsets k_scan uses (its slots' LDS-DMA bases below 112 KiB)
+    constexpr uint32_t kScanLds = kGearLdsBytes + kS2Waves * kStageBytes;
+    __shared__ __attribute__((aligned(16))) char s_all[kScanLds + 256 * kWCopies * 8 + kS2Waves * kGExtra * 8];
+    char *const s_lds = s_all;
+    uint64_t *const s_wtab = reinterpret_cast<uint64_t *>(s_all + kScanLds);
+    uint64_t *const s_gx0 = s_wtab + 256 * kWCopies;  // wave w's graph bits and nodes at s_gx0 + w kGExtra
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
@@ -2114,25 +2197,43 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_chunk(const Batch B, const De
     for (uint32_t k = 0; k < kTiers; ++k) {
         const uint32_t tr = tier + k < kTiers ? tier + k : tier + k - kTiers;
         for (;;) {
-            uint32_t i = 0;
-            if (lane == 0) i = __hip_atomic_fetch_add(W.tick + 3 + tr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            i = __builtin_amdgcn_readfirstlane(i);
+            const uint32_t i = wave_ticket(W.tick + 3 + tr);
             const uint32_t task = tr * tpt + i;
             if (i >= tpt || task >= T) break;
-            scan_task<false, false, true>(B, P, W, s_lds, s_lds, task, lane, wave, laneoff);
+            const uint64_t ts0 = (B.debug & kDbgTs) ? __builtin_amdgcn_s_memrealtime() : 0;
+            scan_task<false, kFused, true>(B, P, W, s_lds, s_lds, task, lane, wave, laneoff);
             drain_stores();
             if (lane == 0) __hip_atomic_store(W.tdone + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((B.debug & kDbgTs) && lane == 0 && task < kTsTasks) {
+                uint64_t *o = g_ts + kTsTask + 4 * task;
+                o[0] = ts0;
+                o[1] = __builtin_amdgcn_s_memrealtime();
+                o[2] = wave;
+                o[3] = uint64_t(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11))) << 32 |
+                       uint32_t(__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)));
+            }
         }
     }
     __builtin_amdgcn_s_setprio(0);
-    const GraphLds L = graph_lds(s_lds + kGearLdsBytes + wave * kStageBytes, s_gx[wave]);
+    if (B.debug & kDbgScanOnly) return;
+    const GraphLds L = graph_lds(s_lds + kGearLdsBytes + wave * kStageBytes, s_gx0 + wave * kGExtra);
     for (;;) {
-        uint32_t g = 0;
-        if (lane == 0) g = __hip_atomic_fetch_add(W.tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        g = __builtin_amdgcn_readfirstlane(g);
+        const uint32_t g = wave_ticket(W.tick);
         if (g >= B.total_segs) break;
         resolve_segment<true>(B, P, W, g, reinterpret_cast<const char *>(s_wtab), L);
     }
+}
+
+__global__ __launch_bounds__(kS2Waves * 64) void k_chunk(const Batch B, const DevParams P, const Workspace W)
+{
+    chunk_body<false>(B, P, W);
+}
+
+// k_chunk with both indexes built in the scan (k_scan_f's body): a launch
+// group that needs the MaskL index, where the masks admit the fused window.
+__global__ __launch_bounds__(kS2Waves * 64) void k_chunk_f(const Batch B, const DevParams P, const Workspace W)
+{
+    chunk_body<true>(B, P, W);
 }
 
 // ---------------------------------------------------------------------------
@@ -2234,7 +2335,7 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_w1_nodes = take(segs * 64 * 8);
     plan->off_xg = take(segs * 8);
     plan->off_sg = take(segs * 8);
-    plan->off_flags = take(kMaxBufsPerLaunch * 4);
+    plan->off_flags = take((kMaxBufsPerLaunch + 4) * 4);  // per buffer + the abort word
     plan->off_tick = take(8 * 4);  // [0] segment ticket, [2] persistent scan task counter, [3..5] k_chunk tiers
     plan->off_tdone = take(tasks * 4);
     plan->off_runsL = take(tasks * 64 * 8);
@@ -2285,12 +2386,18 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
         uint32_t wgs = need_wgs > 0 ? need_wgs : 1u;
         if (B.persist && B.scan_wgs < wgs) wgs = B.scan_wgs;
         if (prof) {
-            hipExtLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
+            if (B.maskl_index)
+                hipExtLaunchKernelGGL(k_chunk_f, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
+            else
+                hipExtLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
             std::lock_guard<std::mutex> lk(g_prof_mu);
             (void)hipEventRecord(pr.e2, st);
             g_prof_live.push_back(pr);
         } else {
-            hipLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, B, P, W);
+            if (B.maskl_index)
+                hipLaunchKernelGGL(k_chunk_f, dim3(wgs), dim3(kS2Waves * 64), 0, st, B, P, W);
+            else
+                hipLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, B, P, W);
         }
         // the adaptive MaskL probe reads this launch's records; it only sets the hint for later groups
         if (B.total_tasks > 0 && B.maskl_probe)

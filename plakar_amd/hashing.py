@@ -102,6 +102,41 @@ def chunk_digests_batch(datas, cut_lists, results=None, hist=True, stream=None):
     return outs
 
 
+def chunk_digests_hybrid(datas, cut_lists, results=None, hist=True, stream=None, host_threads=16,
+                         host_min_len=0):
+    """chunk_digests_batch() with the longest chunks' SHA-256 on host cores
+    (cdc_chunk_digests_hybrid): a device chain costs ~2 us per 64-B block, a
+    host core with the SHA extensions ~35 ns, and one device launch lasts as
+    long as its longest chunk.  Synchronous.  Returns (outs, host_chunks,
+    host_bytes), outs as chunk_digests_batch's."""
+    n = len(datas)
+    if n == 0:
+        return [], 0, 0
+    if n > 32:
+        raise ValueError("at most 32 buffers")
+    dev = datas[0].device
+    for t, c in zip(datas, cut_lists):
+        if t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("expected contiguous uint8 CUDA tensors")
+        if c.dtype != torch.int64 or c.dim() != 2 or c.shape[1] != 2 or not c.is_contiguous():
+            raise ValueError("expected (n, 2) contiguous int64 cut tensors")
+    outs = [(torch.empty((c.shape[0], 32), dtype=torch.uint8, device=dev),
+             torch.empty((c.shape[0], 256), dtype=torch.int32, device=dev) if hist else None) for c in cut_lists]
+    V = ctypes.c_void_p
+    arr = lambda xs: (V * n)(*xs)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    hc, hb = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().cdc_chunk_digests_hybrid(
+        dev.index, arr([t.data_ptr() for t in datas]), (ctypes.c_uint64 * n)(*[t.numel() for t in datas]), n,
+        arr([c.data_ptr() for c in cut_lists]), (ctypes.c_uint64 * n)(*[c.shape[0] for c in cut_lists]),
+        arr([r.data_ptr() for r in results]) if results is not None else None,
+        arr([o[0].data_ptr() for o in outs]), arr([o[1].data_ptr() for o in outs]) if hist else None,
+        int(host_threads), int(host_min_len), V(stream.cuda_stream), ctypes.byref(hc), ctypes.byref(hb)),
+        "hybrid digests")
+    return outs, int(hc.value), int(hb.value)
+
+
 def chunk_entropy_device(hist, stream=None):
     """entropy() per histogram row on the device (cdc_chunk_entropy_device_async):
     hist is a (n, 256) int32/uint32 CUDA tensor as chunk_digests returns it;

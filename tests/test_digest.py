@@ -221,6 +221,63 @@ def test_gpu_digest_batch_many_buffers():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("host_min_len", [0, 1, 30000, 1 << 40])
+def test_gpu_digest_hybrid_matches_hashlib(host_min_len):
+    """cdc_chunk_digests_hybrid: the longest chunks' SHA-256 on host cores,
+    the rest and every histogram on the device; every row equals hashlib /
+    bincount whatever the split (0: the library's balance, 1: every non-empty
+    chunk on the host, 1 << 40: none), over several buffers with unaligned
+    chunks, empty ones, gaps and result rows that bound the counts."""
+    torch = _gpu()
+    from plakar_amd import _lib, hashing
+    _lib.ensure_init()
+    bufs, cut_lists, res, refs = [], [], [], []
+    for k in range(4):
+        data = random_bytes(3_000_000 + 104729 * k, 60 + k)
+        cuts, o = [], k
+        while o + 70000 < data.size:
+            n = int((o * 2654435761) % 60000) + (40000 if (o // 7) % 5 == 0 else 0)
+            n = min(n, data.size - o)
+            cuts.append((o, n))
+            o += n + (o % 3)
+        cuts.append((0, 0))
+        keep = len(cuts) - 2 if k % 2 else len(cuts)
+        bufs.append(torch.from_numpy(data).cuda())
+        cut_lists.append(torch.tensor(np.asarray(cuts, np.int64), device="cuda"))
+        res.append(torch.tensor([keep, 0, 0, 0], dtype=torch.int64, device="cuda"))
+        refs.append((data, cuts[:keep]))
+    outs, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res, host_threads=8, host_min_len=host_min_len)
+    torch.cuda.synchronize()
+    for (data, cuts), (d, h) in zip(refs, outs):
+        _check(data, cuts, d[:len(cuts)].cpu().numpy(), h[:len(cuts)].cpu().numpy())
+    nonempty = sum(1 for _, cuts in refs for _, n in cuts if n)
+    if host_min_len == 1:
+        assert hc == nonempty and hb == sum(n for _, cuts in refs for _, n in cuts)
+    elif host_min_len == 1 << 40:
+        assert hc == 0 and hb == 0
+    else:
+        assert 0 <= hc <= nonempty
+
+
+@pytest.mark.gpu
+def test_gpu_digest_hybrid_c1_pass():
+    """The hybrid split on a C1 pass (1 GiB random, the device's own cut
+    lists): digests equal the device-only path's, and some chunks went to
+    the host."""
+    torch = _gpu()
+    from plakar_amd import _lib, chunkers, device, hashing
+    _lib.ensure_init()
+    t = torch.from_numpy(random_bytes(1 << 30, 1)).cuda()
+    b = device.DeviceBatch([t], chunkers.ChunkerOpts(65536, 1 << 20, 4 << 20))
+    b.launch()
+    (d0, h0), = hashing.chunk_digests_batch([t], [b.cuts[0]], [b.res[0]])
+    (d1, h1), = hashing.chunk_digests_hybrid([t], [b.cuts[0]], [b.res[0]], host_threads=16)[0]
+    torch.cuda.synchronize()
+    n = int(b.results()[1][0, 0])
+    assert torch.equal(d0[:n], d1[:n]) and torch.equal(h0[:n], h1[:n])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lanes", [1, 3, 64, 100])
 def test_gpu_digest_multi_chunk_lanes(lanes):
     """A launch with more chunks than resident lanes gives each lane a run of
