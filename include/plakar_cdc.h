@@ -466,10 +466,11 @@ int cdc_set_debug_mode(int mode);
  * CDC_E_INVALID. */
 int cdc_set_maskl_index_mode(int mode);
 
-/* How a launch group resolves its cut points: 1 = in the same launch as the
- * scan (k_chunk, the default wherever the group needs no MaskL index), 0 =
- * always by a second launch (k_scan + k_resolve).  Cut points never depend on
- * it; tests run both.  Initial value from the CDC_RESOLVE_MODE environment
+/* How a launch group resolves its cut points: 0 = by a second launch after
+ * the scan (k_scan + k_resolve, the default), 1 = in the same launch as the
+ * scan (k_chunk / k_chunk_f, where the MaskL index does not need k_scan_l;
+ * measured slower).  Cut points never depend on it; the GPU
+ * tests run both.  Initial value from the CDC_RESOLVE_MODE environment
  * variable.  Not a reference interface.  Returns CDC_OK or CDC_E_INVALID. */
 int cdc_set_resolve_mode(int mode);
 

@@ -90,13 +90,16 @@ Global &G()
 }
 
 // Resolution mode (cdc_set_resolve_mode; initial value from CDC_RESOLVE_MODE):
-// 1 the scan and the resolution in one launch (k_chunk) wherever the launch
-// group needs no MaskL index, 0 always two launches (k_scan + k_resolve).
+// 0 two launches (k_scan + k_resolve, the default), 1 the scan and the
+// resolution in one launch (k_chunk / k_chunk_f) wherever the MaskL index
+// does not need k_scan_l.  One launch measured slower (DESIGN.md 5.3,
+// profiles/r05_one_launch_ab.txt): its resolution waves, at 168 VGPRs with
+// spills, slow the last scan tasks.
 std::atomic<uint32_t> &resolve_mode()
 {
     static std::atomic<uint32_t> m([] {
         const char *e = getenv("CDC_RESOLVE_MODE");
-        return e && e[0] == '0' ? 0u : 1u;
+        return e && e[0] == '1' ? 1u : 0u;
     }());
     return m;
 }

@@ -86,7 +86,8 @@ struct Workspace {
     uint64_t *xg;        // [total_segs] granule: published | node count | speculative exit X_q
     uint64_t *sg;        // [total_segs] granule: LOCAL (conv, cuts) or INCLUSIVE (E, O)
     uint32_t *flags;     // [kMaxBufsPerLaunch + 4] per-buffer "resolve sequentially", then the abort word
-    uint32_t *tick;      // [8] [0] segment ticket, [2] persistent scan task counter, [3..5] k_chunk tier counters
+    uint32_t *tick;      // [16 + tasks] [0] segment ticket, [2] persistent scan task counter, [8..16) k_chunk "tasks
+                         // taken" shards, [16..) k_chunk per-task claims
     // k_chunk: per scan task, 1 once its run records are stored (write-through)
     // and readable by another workgroup.  xg .. tdone is one contiguous range,
     // zeroed before every k_chunk launch.

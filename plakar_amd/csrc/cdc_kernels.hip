@@ -2174,6 +2174,29 @@ constexpr uint32_t kTiers = 3;
 static_assert(kS2Waves % kTiers == 0, "tiers of whole SIMD rounds");
 static_assert(kGRecs * 8 <= kStageBytes, "a wave's graph records fit its scan slot");
 
+// Claim word p for this wave: every lane takes part (lane 0 ORs 1, the
+// others 0, so no lane-0 branch precedes the readfirstlane, see wave_ticket);
+// true if this wave set it.
+__device__ __forceinline__ bool wave_claim(uint32_t *p)
+{
+    const uint32_t old = __hip_atomic_fetch_or(p, (threadIdx.x & 63u) == 0u ? 1u : 0u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(old) == 0u;
+}
+
+constexpr uint32_t kStartShards = 8;  // k_chunk: "tasks taken" counter, sharded by task % 8 (tick[8 .. 16))
+constexpr uint32_t kTickClaims = 16;  // k_chunk: per-task claim words from tick[16]
+
+__device__ __forceinline__ uint32_t tasks_taken(const uint32_t *shards)
+{
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t v = l < kStartShards ? __hip_atomic_load(shards + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t sum = v;
+#pragma unroll
+    for (int o = 4; o; o >>= 1) sum += uint32_t(__shfl_xor(int(sum), o));
+    return __builtin_amdgcn_readfirstlane(sum);
+}
+
 template <bool kFused>
 __device__ __forceinline__ void chunk_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
@@ -2187,34 +2210,76 @@ __device__ __forceinline__ void chunk_body(const Batch &B, const DevParams &P, c
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
+    const uint32_t T = B.total_tasks;
+    uint32_t *const shards = W.tick + 8;
+    uint32_t *const claim = W.tick + kTickClaims;
+    // Static ownership: workgroup w's wave j owns task tier(j) tpt + 4 w +
+    // j % 4 (tier k = wave age k on its SIMD; tier k holds the k-th third of
+    // the tasks).  The claim (a word per task, no contention) flies while the
+    // tables fill.
+    constexpr uint32_t kPerTier = kS2Waves / kTiers;
+    const uint32_t tpt = gridDim.x * kPerTier;
+#ifdef CDC_CHUNK_MAP_LINEAR
+    const uint32_t mine = blockIdx.x * kS2Waves + wave;  // build-time A/B: k_scan's mapping
+    (void)tpt;
+#else
+    const uint32_t mine = (wave / kPerTier) * tpt + blockIdx.x * kPerTier + wave % kPerTier;
+#endif
+    bool own = false;
+    if (mine < T) own = wave_claim(claim + mine);
     fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, P.fs_sh);
     fill_gear_lds<kS2Waves * 64, kWCopies>(s_wtab, W.gear);
     if (blockIdx.x == 0 && wave == 0) write_empty_rows(B, lane);
     __syncthreads();
+#ifndef CDC_CHUNK_NO_PRIO
     __builtin_amdgcn_s_setprio(1);
-    const uint32_t T = B.total_tasks, tpt = (T + kTiers - 1) / kTiers;
-    const uint32_t tier = wave / (kS2Waves / kTiers);
-    for (uint32_t k = 0; k < kTiers; ++k) {
-        const uint32_t tr = tier + k < kTiers ? tier + k : tier + k - kTiers;
-        for (;;) {
-            const uint32_t i = wave_ticket(W.tick + 3 + tr);
-            const uint32_t task = tr * tpt + i;
-            if (i >= tpt || task >= T) break;
-            const uint64_t ts0 = (B.debug & kDbgTs) ? __builtin_amdgcn_s_memrealtime() : 0;
-            scan_task<false, kFused, true>(B, P, W, s_lds, s_lds, task, lane, wave, laneoff);
-            drain_stores();
-            if (lane == 0) __hip_atomic_store(W.tdone + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((B.debug & kDbgTs) && lane == 0 && task < kTsTasks) {
-                uint64_t *o = g_ts + kTsTask + 4 * task;
-                o[0] = ts0;
-                o[1] = __builtin_amdgcn_s_memrealtime();
-                o[2] = wave;
-                o[3] = uint64_t(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11))) << 32 |
-                       uint32_t(__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)));
-            }
+#endif
+    auto scan_one = [&](uint32_t task) {
+        if (lane == 0) __hip_atomic_fetch_add(shards + task % kStartShards, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t ts0 = (B.debug & kDbgTs) ? __builtin_amdgcn_s_memrealtime() : 0;
+        scan_task<false, kFused, true>(B, P, W, s_lds, s_lds, task, lane, wave, laneoff);
+        drain_stores();
+        if (lane == 0) __hip_atomic_store(W.tdone + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((B.debug & kDbgTs) && lane == 0 && task < kTsTasks) {
+            uint64_t *o = g_ts + kTsTask + 4 * task;
+            o[0] = ts0;
+            o[1] = __builtin_amdgcn_s_memrealtime();
+            o[2] = wave;
+            o[3] = uint64_t(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11))) << 32 |
+                   uint32_t(__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)));
         }
+    };
+    if (own) scan_one(mine);
+    // Every task must be taken by a running wave before any walker waits: a
+    // task whose workgroup is not yet dispatched (its CU held by another
+    // stream's kernel) is taken by a wave that is done (only under such
+    // contention; the counter's adds fly while the tasks are scanned).
+    for (SpinGuard sp;;) {
+        if (tasks_taken(shards) >= T) break;
+        bool took = false;
+        for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            const uint32_t c = t < T ? __hip_atomic_load(claim + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+            uint64_t m = __ballot(c == 0u);
+            while (m) {
+                const uint32_t v = t0 + uint32_t(__ffsll((unsigned long long)m) - 1);
+                m &= m - 1;
+                if (wave_claim(claim + v)) {
+                    scan_one(v);
+                    took = true;
+                    break;
+                }
+            }
+            if (took) break;
+        }
+        if (took) continue;
+        if (!sp.ok(W.flags, kWaitTask, T, 0)) break;  // every task claimed, the count not yet seen
+        __builtin_amdgcn_s_sleep(kSpinSleep);
     }
-    __builtin_amdgcn_s_setprio(0);
+    // the walkers' latency-bound work issues ahead of the remaining scans
+#ifndef CDC_CHUNK_NO_PRIO
+    __builtin_amdgcn_s_setprio(2);
+#endif
     if (B.debug & kDbgScanOnly) return;
     const GraphLds L = graph_lds(s_lds + kGearLdsBytes + wave * kStageBytes, s_gx0 + wave * kGExtra);
     for (;;) {
@@ -2336,7 +2401,9 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_xg = take(segs * 8);
     plan->off_sg = take(segs * 8);
     plan->off_flags = take((kMaxBufsPerLaunch + 4) * 4);  // per buffer + the abort word
-    plan->off_tick = take(8 * 4);  // [0] segment ticket, [2] persistent scan task counter, [3..5] k_chunk tiers
+    // [0] segment ticket, [2] persistent scan task counter, [8 .. 16) k_chunk
+    // "tasks taken" shards, [16 ..] k_chunk per-task claims
+    plan->off_tick = take((16 + tasks) * 4);
     plan->off_tdone = take(tasks * 4);
     plan->off_runsL = take(tasks * 64 * 8);
     plan->off_validL = take(tasks * 4);
@@ -2383,8 +2450,9 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     if (B.one_launch) {  // k_chunk: counters, flags and granules zeroed, then one kernel
         const size_t zb = size_t(reinterpret_cast<char *>(W.tdone + B.total_tasks) - reinterpret_cast<char *>(W.xg));
         if (hipMemsetAsync(W.xg, 0, zb, st) != hipSuccess) return CDC_E_DEVICE;
-        uint32_t wgs = need_wgs > 0 ? need_wgs : 1u;
-        if (B.persist && B.scan_wgs < wgs) wgs = B.scan_wgs;
+        // one task per wave (a late workgroup's tasks are taken by waves that
+        // are done, so the grid needs no persistent form)
+        const uint32_t wgs = need_wgs > 0 ? need_wgs : 1u;
         if (prof) {
             if (B.maskl_index)
                 hipExtLaunchKernelGGL(k_chunk_f, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);

@@ -96,9 +96,9 @@ def set_maskl_index_mode(mode):
 
 
 def set_resolve_mode(mode):
-    """1 = the scan and the chain resolution in one launch (k_chunk, the
-    default wherever a launch group needs no MaskL index), 0 = always two
-    launches (k_scan + k_resolve). Cut points do not depend on it."""
+    """0 = two launches (k_scan + k_resolve, the default), 1 = the scan and
+    the chain resolution in one launch (k_chunk; measured slower, DESIGN.md
+    5.3). Cut points do not depend on it."""
     check(lib().cdc_set_resolve_mode(int(mode)))
 
 

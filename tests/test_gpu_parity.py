@@ -61,7 +61,7 @@ _MASKL_MODE = int(_MASKL_ENV) if _MASKL_ENV in ("0", "1", "2", "3") else 1
 
 
 # the suite's resolution mode (CDC_RESOLVE_MODE), restored after each test
-_RESOLVE_MODE = 0 if os.environ.get("CDC_RESOLVE_MODE", "1")[:1] == "0" else 1
+_RESOLVE_MODE = 1 if os.environ.get("CDC_RESOLVE_MODE", "0")[:1] == "1" else 0
 
 
 @pytest.fixture(params=[1, 0], ids=["one-launch", "two-launch"])

@@ -64,8 +64,11 @@ def main():
     r = r[r[:, 4] > 0]
     if len(tk):
         t0 = tk[:, 0].min()
-    else:
+    elif len(r):
         t0 = r[:, 0].min()
+    else:
+        print("no stamps")
+        return
     us = lambda x: (x - t0) / 100.0
     if len(tk):
         print(f"scan tasks {len(tk)}: start {pct(us(tk[:, 0]))}")
@@ -75,7 +78,16 @@ def main():
             sel = (tk[:, 2] // 4) == tier
             if sel.any():
                 print(f"  tier {tier} (waves {4 * tier}-{4 * tier + 3}): {int(sel.sum())} tasks, end {pct(us(tk[sel, 1]))}")
+    if len(r) == 0:
+        print(f"no segment stamps; last scan task end {us(tk[:, 1].max()) if len(tk) else float('nan'):.1f} us")
+        return
     print(f"segments {len(r)}: start {pct(us(r[:, 0]))}")
+    third = len(r) // 3
+    for k in range(3):
+        sel = slice(k * third, (k + 1) * third if k < 2 else len(r))
+        rr = r[sel]
+        print(f"  segments {k}/3: start {pct(us(rr[:, 0]), (50, 100))}  built {pct(us(rr[:, 1]), (50, 100))}  "
+              f"inclusive {pct(us(rr[:, 4]), (50, 100))}")
     print(f"  graph built {pct(us(r[:, 1]))}   (built - start) {pct((r[:, 1] - r[:, 0]) / 100.0)}")
     print(f"  spec exit {pct(us(r[:, 2]))}   (- built) {pct((r[:, 2] - r[:, 1]) / 100.0)}")
     lb = r[1:, 3]
