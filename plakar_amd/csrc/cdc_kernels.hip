@@ -295,7 +295,10 @@ struct SpinGuard {
 // exact recheck then ignores.
 // ---------------------------------------------------------------------------
 
-constexpr uint32_t kS2Waves = 12;                     // waves per scan workgroup (one workgroup per CU)
+#ifndef CDC_SCAN_WAVES
+#define CDC_SCAN_WAVES 12
+#endif
+constexpr uint32_t kS2Waves = CDC_SCAN_WAVES;         // waves per scan workgroup (one workgroup per CU)
 constexpr uint32_t kStage = 64;                       // bytes per lane per stage
 constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane per stage = DMAs per stage
 constexpr uint32_t kGroups = kStage / 16;             // 16-byte groups per stage
@@ -2170,8 +2173,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B,
 // slot then holds its graph's run records), the walkers' 16-KiB table, and
 // 12 x 1,088 B of graph bits and nodes: 141 KiB.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kTiers = 3;
-static_assert(kS2Waves % kTiers == 0, "tiers of whole SIMD rounds");
+constexpr uint32_t kTiers = kS2Waves % 3 == 0 ? 3 : 1;
 static_assert(kGRecs * 8 <= kStageBytes, "a wave's graph records fit its scan slot");
 
 // Claim word p for this wave: every lane takes part (lane 0 ORs 1, the
