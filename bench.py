@@ -50,6 +50,10 @@ WORKLOADS = {
                      "points, chunk SHA-256 + histograms, BlobExists, Encode (LZ4 + AES-256-GCM, random key), 8 "
                      "concurrent packers -> packfiles (20 MiB); every file, small ones included; warm page cache",
                 nbuf=512, size=0, kind="zipf", host=True, files=True, backup=True),
+    "c4bl": dict(desc="c4b over large files: 4 files of 1536 / 1280 / 768 / 520 MiB (each several device batches, "
+                      "so every file is backed up in pieces) and 60 Zipf files of the C4 distribution; same pipeline",
+                 nbuf=64, size=0, kind="zipf", host=True, files=True, backup=True,
+                 large_mib=(1536, 1280, 768, 520)),
 }
 
 
@@ -104,6 +108,9 @@ def make_host_corpus(wl, rank, world):
     """C4: the rank's share of the corpus as pageable host buffers (uniform bytes)."""
     import numpy as np
     sizes = zipf_sizes(wl["nbuf"] * world, 300)[rank * wl["nbuf"]:(rank + 1) * wl["nbuf"]]
+    large = [m << 20 for m in wl.get("large_mib", ())]
+    if large:  # c4bl: the large files first, then Zipf files to nbuf
+        sizes = list(large) + list(sizes[:wl["nbuf"] - len(large)])
     out = []
     for seed, n in zip(buffer_seeds(wl, rank, world), sizes):
         n = int(n)
