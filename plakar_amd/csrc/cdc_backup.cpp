@@ -1191,26 +1191,14 @@ int cdc_backup_new(int device, const cdc_backup_opts *opts, cdc_backup **out)
     }
     if (const char *q = std::getenv("GPU_MAX_HW_QUEUES")) b->hw_queues = std::atoi(q);
     bool ok = hipSetDevice(device) == hipSuccess;
-    // The digest streams run on every other CU: a digest launch holds its
-    // CUs' LDS for its longest chain (10-18 ms per batch, two in flight), and
-    // a scan or k_gcm workgroup (112 / 148 KiB of LDS) cannot sit beside one,
-    // so on an unmasked device the other kernels' last workgroups waited for
-    // the digests to end (Encode of a batch: 12 ms alone, 30-55 ms beside
-    // them, profiles/r04_c4b_trace.txt).  CDC_BACKUP_DIGEST_CUS=all lifts it.
-    int cus = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    const char *dm = std::getenv("CDC_BACKUP_DIGEST_CUS");
-    const bool mask_digests = cus >= 64 && !(dm && std::string(dm) == "all");
-    for (int i = 0; i < int(sizeof(b->stream) / sizeof(b->stream[0])); ++i) {
-        hipStream_t &sm = b->stream[i];
-        if (ok && mask_digests && (i == kD || i == kD + 1)) {
-            std::vector<uint32_t> m(size_t((cus + 31) / 32), 0u);
-            for (int c = 0; c < cus; c += 2) m[size_t(c / 32)] |= 1u << (c % 32);
-            if (hipExtStreamCreateWithCUMask(&sm, uint32_t(m.size()), m.data()) == hipSuccess) continue;
-            sm = nullptr;  // no CU masks here: an ordinary stream
-        }
-        ok = ok && hipStreamCreateWithFlags(&sm, hipStreamNonBlocking) == hipSuccess;
-    }
+    // Every stream non-blocking.  Round 4 put the two digest streams on every
+    // other CU (hipExtStreamCreateWithCUMask); measured in round 5, the mask
+    // does not restrict placement on this ROCm (a masked stream's workgroups
+    // ran on all 256 CUs) and such a stream blocks on the legacy null stream
+    // (profiles/r05z_cu_mask_probe.txt, tools/cu_mask_probe.hip); c4b was the
+    // same either way (profiles/r05_c4b_cu_mask_ab.txt), so it is gone.
+    for (int i = 0; i < int(sizeof(b->stream) / sizeof(b->stream[0])); ++i)
+        ok = ok && hipStreamCreateWithFlags(&b->stream[i], hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         cdc_backup_free(b);
         return CDC_E_DEVICE;
