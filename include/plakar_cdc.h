@@ -208,8 +208,10 @@ void cdc_packer_free(cdc_packer *p);
  * threads append the blobs to their own packfiles and hand each one, at
  * Size() > packfile_max (0: 20 MiB) and at the end, to on_pack (PutPackfile;
  * calls are serialised, from packer threads).  on_file is called once per
- * file, largest files first (the order the pipeline processes them: a large
- * file's object hash is a long serial chain), from one library thread (the
+ * file (per piece, below) in the order the pipeline processes them: every
+ * file's first piece, largest file first (a large file's object hash is a
+ * long serial chain), then the later pieces of large files round by round,
+ * so pieces of different files interleave; from one library thread (the
  * calling thread meanwhile
  * drives the next batches through the device), with pointers valid during the
  * call only; chunk entropies come from the device (cdc_chunk_entropy_device_async).

@@ -417,8 +417,13 @@ int plan(Run &R, uint64_t &arena_cap, uint64_t &cuts_cap, uint64_t &ws_cap, uint
     // host core (a 128-MiB file ~64 ms) and a slot is released only once
     // every hash of its batch is done, so a large file late in the run held
     // the device idle behind its hash (profiles/r03_c4b_timeline.txt: gaps of
-    // 15-70 ms).  Pieces of one file stay consecutive; callbacks come in this
-    // processing order (each names its file).
+    // 15-70 ms).  Pieces go round by round: every file's piece 0 (largest
+    // file first), then every piece 1, and so on.  Piece j + 1 can only be
+    // hashed after piece j, so with a large file's pieces consecutive its
+    // later pieces held slots for seconds while the next large file waited
+    // for one (c4bl: 4 files of 0.5-1.5 GiB hashed one after another, 1.24 s;
+    // round by round their chains run side by side).  Callbacks come in this
+    // processing order (each names its file and piece).
     {
         std::vector<uint32_t> first(size_t(R.n) + 1, 0);  // units of file i: [first[i], first[i + 1])
         for (size_t u = 0; u < R.units.size(); ++u) first[R.units[u].file + 1] = uint32_t(u + 1);
@@ -429,8 +434,14 @@ int plan(Run &R, uint64_t &arena_cap, uint64_t &cuts_cap, uint64_t &ws_cap, uint
                          [&](uint32_t a, uint32_t b) { return R.files[a].size > R.files[b].size; });
         std::vector<Unit> sorted;
         sorted.reserve(R.units.size());
-        for (uint32_t i : ord)
-            for (uint32_t u = first[i]; u < first[i + 1]; ++u) sorted.push_back(R.units[u]);
+        std::vector<uint32_t> multi;  // files in pieces, largest first
+        for (uint32_t i : ord) {
+            sorted.push_back(R.units[first[i]]);  // round 0: every file (a file has at least one unit)
+            if (first[i + 1] - first[i] > 1) multi.push_back(i);
+        }
+        for (uint32_t r = 1; sorted.size() < R.units.size(); ++r)
+            for (uint32_t i : multi)
+                if (first[i] + r < first[i + 1]) sorted.push_back(R.units[first[i] + r]);
         R.units.swap(sorted);
     }
     R.batch_of.resize(R.units.size());
