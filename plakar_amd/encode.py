@@ -12,6 +12,23 @@ from . import _lib
 from ._lib import check, ensure_init, lib
 
 RANDOM_BYTES = 56  # per blob: subkey 32, subkey nonce 12, data nonce 12
+_URANDOM_SPLIT = 256 << 10  # above this, os.urandom in parallel pieces
+_urandom_pool = None
+
+
+def _urandom(n):
+    """os.urandom(n); a large draw (a batch of ~20 K blobs needs 1.2 MB, ~4 ms
+    from one thread) in four pieces on threads (getrandom releases the GIL):
+    the same kernel CSPRNG, ~2x sooner."""
+    global _urandom_pool
+    if n <= _URANDOM_SPLIT:
+        return os.urandom(n)
+    if _urandom_pool is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _urandom_pool = ThreadPoolExecutor(4, thread_name_prefix="plakar-urandom")
+    k = 4
+    sizes = [n // k + (1 if i < n % k else 0) for i in range(k)]
+    return b"".join(_urandom_pool.map(os.urandom, sizes))
 
 
 def encode_bound(n, compress=True, encrypt=True):
@@ -37,7 +54,7 @@ def encode_device(base, offsets, lens, out, key=None, compress=True, random=None
         if len(key) != 32:
             raise ValueError("the repository key is 32 bytes (AES-256)")
         if random is None:
-            random = os.urandom(RANDOM_BYTES * n)
+            random = _urandom(RANDOM_BYTES * n)
         if len(random) != RANDOM_BYTES * n:
             raise ValueError(f"random: {RANDOM_BYTES} bytes per blob")
     st = stream if stream is not None else torch.cuda.current_stream(device)
