@@ -354,6 +354,7 @@ class BackupSession:
         pending = {}  # file index -> ChunkRecords of its pieces so far (files larger than batch_bytes)
         ctypes_of = {}  # file index -> ContentType (from its first piece)
         self.failed = {}  # file index -> status of the files that could not be read (recordError)
+        self.callback_order = []  # (file index, piece) in the order the pipeline delivered them
         packs = []
         errors = []
 
@@ -366,6 +367,7 @@ class BackupSession:
             try:
                 f = fp.contents
                 i = int(f.index)
+                self.callback_order.append((i, int(f.piece)))
                 if f.status != 0:  # backupCtx.recordError (snapshot/backup.go:264-267): no object, the run goes on
                     self.failed[i] = int(f.status)
                     pending.pop(i, None)

@@ -158,6 +158,36 @@ def test_backup_files_larger_than_the_batch_go_in_pieces(tmp_path):
     assert set(_blobs_of(packs, KEY, True)) == {c.Checksum for o in objs for c in o.Chunks}
 
 
+def test_backup_pieces_of_large_files_go_round_by_round(tmp_path):
+    """Every file's first piece comes first (largest file first), then the
+    later pieces round by round, so the object hashes of several large files
+    (one serial chain each) run side by side; a file's pieces still arrive in
+    order and the objects equal the whole-file path's."""
+    sizes = [50 << 20, 40 << 20, 3 << 20, 35 << 20]
+    files = [random_bytes(n, 61 + i).tobytes() for i, n in enumerate(sizes)]
+    paths = []
+    for i, b in enumerate(files):
+        p = tmp_path / f"r{i}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    with snapshot.BackupSession(key=KEY, batch_bytes=8 << 20, packers=2) as s:
+        objs, _, st = s.run(paths)
+        order = list(s.callback_order)
+    piece = 4 * (4 << 20)  # max(batch_bytes, 4 Max)
+    npieces = [-(-n // piece) if n > piece else 1 for n in sizes]
+    assert sorted(order) == sorted((i, j) for i, k in enumerate(npieces) for j in range(k))
+    assert [i for i, j in order if j == 0] == [0, 1, 3, 2]  # round 0, largest first
+    rounds = [j for _, j in order]
+    assert rounds == sorted(rounds)  # round by round
+    for i in range(len(files)):
+        assert [j for f, j in order if f == i] == list(range(npieces[i]))
+    ref = snapshot.chunkify_batch(files)
+    for o, r, b in zip(objs, ref, files):
+        assert o.Checksum == r.Checksum == hashlib.sha256(b).digest()
+        assert [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks]
+    assert st["failed_files"] == 0
+
+
 def test_backup_large_file_failing_in_a_middle_piece(tmp_path, monkeypatch):
     """A file in pieces whose third piece cannot be read (the library's test
     hook CDC_BACKUP_FAIL_PIECE=file:piece, as a file that shrank mid-run):
