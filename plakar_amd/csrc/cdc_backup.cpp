@@ -1206,7 +1206,7 @@ int cdc_backup_new(int device, const cdc_backup_opts *opts, cdc_backup **out)
     // other CU (hipExtStreamCreateWithCUMask); measured in round 5, the mask
     // does not restrict placement on this ROCm (a masked stream's workgroups
     // ran on all 256 CUs) and such a stream blocks on the legacy null stream
-    // (profiles/r05z_cu_mask_probe.txt, tools/cu_mask_probe.hip); c4b was the
+    // (profiles/r05final_cu_mask_probe.txt, tools/cu_mask_probe.hip); c4b was the
     // same either way (profiles/r05_c4b_cu_mask_ab.txt), so it is gone.
     for (int i = 0; i < int(sizeof(b->stream) / sizeof(b->stream[0])); ++i)
         ok = ok && hipStreamCreateWithFlags(&b->stream[i], hipStreamNonBlocking) == hipSuccess;
