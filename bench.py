@@ -149,6 +149,25 @@ def load_traffic(workload):
         return None
 
 
+def stream_read_peak(torch, L, bufs, dev, local, reps=20):
+    """The device's measured HBM stream-read rate (report it
+    beside the 8 TB/s spec), in the same clock state as the roofline loop it
+    follows: k_stream_read over 1 GiB (the first buffer when it is that large,
+    else a scratch tensor, so the Infinity Cache does not serve it), `reps`
+    launches, best and median."""
+    import ctypes
+    n = 1 << 30
+    src = bufs[0] if bufs[0].numel() >= n else torch.empty(n, dtype=torch.uint8, device=dev)
+    best, med = ctypes.c_double(), ctypes.c_double()
+    st = L.cdc_debug_stream_read(local, ctypes.c_void_p(src.data_ptr()), n, reps, ctypes.byref(best),
+                                 ctypes.byref(med), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    if st != 0 or best.value <= 0:
+        return dict(error=int(st))
+    return dict(best_GBps=round(n / (best.value * 1e-6) / 1e9, 1), median_GBps=round(n / (med.value * 1e-6) / 1e9, 1),
+                bytes=n, reps=reps, kernel="k_stream_read (cdc_debug_stream_read): 16-B loads, four in flight per lane",
+                note="measured after the roofline loop; frac_of_measured_peak = achieved / best_GBps")
+
+
 def digest_leg(torch, batch, bufs, reps, check):
     """Per-chunk SHA-256 + byte histogram (processChunk, snapshot/backup.go:594-629)
     over the device cut lists of the pass: device-resident, events around the
@@ -881,6 +900,11 @@ def main():
                     algorithmic_bytes_per_launch=int(bytes_per_launch),
                     timed_passes=n,
                     pipeline_avg_ms=round(pipe_avg_ms, 4))
+    if not host_mode:
+        roofline["measured_stream_read"] = stream_read_peak(torch, L, bufs, dev, local)
+        best = roofline["measured_stream_read"].get("best_GBps")
+        if best:
+            roofline["frac_of_measured_peak"] = round(achieved / best, 4)
 
     digest = None
     if not host_mode and args.digest_reps > 0:

@@ -859,6 +859,17 @@ int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups)
     return CDC_OK;
 }
 
+int cdc_debug_stream_read(int device, const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us,
+                          void *stream)
+{
+    if (!d_buf || !best_us || !median_us) return CDC_E_INVALID;
+    DeviceCtx *ctx = nullptr;
+    const int st = check_ready(device, &ctx);
+    if (st != CDC_OK) return st;
+    if (hipSetDevice(device) != hipSuccess) return CDC_E_DEVICE;
+    return launch_stream_read(d_buf, len, reps, best_us, median_us, stream);
+}
+
 int cdc_device_count(void)
 {
     int n = 0;

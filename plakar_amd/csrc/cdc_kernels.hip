@@ -28,6 +28,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -2141,6 +2142,73 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B,
     const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(s_ticket)) * kWalkWavesPerWG + wave;
     if (g < B.total_segs)
         resolve_segment<false>(B, P, W, g, reinterpret_cast<const char *>(s_tab), graph_lds(s_grec[wave], s_gx[wave]));
+}
+
+// ---------------------------------------------------------------------------
+// k_stream_read: the HBM stream-read rate SURVEY.md 8(d) asks to report beside
+// the roofline (measured, not the 8 TB/s spec).  Every lane reads 16-byte
+// pieces, four in flight, grid-stride over the buffer, and folds them into
+// one XOR per workgroup (written, so the loads are not dead).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kStreamThreads = 256;
+
+__global__ __launch_bounds__(kStreamThreads) void k_stream_read(const uint4 *p, uint64_t n16, uint32_t *sink)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * kStreamThreads;
+    uint64_t i = uint64_t(blockIdx.x) * kStreamThreads + threadIdx.x;
+    uint32_t x = 0;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) {
+        const uint4 a = p[i];
+        x ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    for (int o = 32; o; o >>= 1) x ^= uint32_t(__shfl_xor(int(x), o));
+    if ((threadIdx.x & 63u) == 0) atomicXor(sink + blockIdx.x, x);
+}
+
+int launch_stream_read(const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us, void *stream)
+{
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint64_t n16 = len / 16;
+    if (n16 == 0 || reps <= 0 || (reinterpret_cast<uintptr_t>(d_buf) & 15u)) return CDC_E_INVALID;
+    int cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return CDC_E_DEVICE;
+    const uint32_t wgs = uint32_t(cus) * 8u;  // 8 workgroups of 4 waves per CU
+    uint32_t *sink = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipMalloc(&sink, wgs * 4) != hipSuccess) return CDC_E_DEVICE;
+    int rc = CDC_OK;
+    std::vector<float> ms;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
+        hipMemsetAsync(sink, 0, wgs * 4, st) != hipSuccess) {
+        rc = CDC_E_DEVICE;
+    } else {
+        for (int r = 0; r < reps && rc == CDC_OK; ++r) {
+            float t = 0.f;
+            const bool rec0 = hipEventRecord(e0, st) == hipSuccess;
+            hipLaunchKernelGGL(k_stream_read, dim3(wgs), dim3(kStreamThreads), 0, st,
+                               static_cast<const uint4 *>(d_buf), n16, sink);
+            const bool rec1 = hipEventRecord(e1, st) == hipSuccess;
+            if (!rec0 || !rec1 || hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&t, e0, e1) != hipSuccess)
+                rc = CDC_E_DEVICE;
+            else
+                ms.push_back(t);
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(sink);
+    if (rc != CDC_OK) return rc;
+    std::sort(ms.begin(), ms.end());
+    if (best_us) *best_us = 1e3 * double(ms.front());
+    if (median_us) *median_us = 1e3 * double(ms[ms.size() / 2]);
+    return CDC_OK;
 }
 
 // ---------------------------------------------------------------------------
