@@ -164,7 +164,7 @@ def stream_read_peak(torch, L, bufs, dev, local, reps=20):
     if st != 0 or best.value <= 0:
         return dict(error=int(st))
     return dict(best_GBps=round(n / (best.value * 1e-6) / 1e9, 1), median_GBps=round(n / (med.value * 1e-6) / 1e9, 1),
-                bytes=n, reps=reps, kernel="k_stream_read (cdc_debug_stream_read): 16-B loads, four in flight per lane",
+                bytes=n, reps=reps, kernel="the fastest of k_stream_read (grid-stride, four 16-B loads in flight per lane), k_stream_read_nt (8-KiB pieces per wave, eight nontemporal 16-B loads per lane) and k_stream_read_lds (the scan's LDS-DMA staging, nothing computed); cdc_debug_stream_read",
                 note="measured after the roofline loop; frac_of_measured_peak = achieved / best_GBps")
 
 

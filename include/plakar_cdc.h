@@ -483,9 +483,10 @@ int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups);
 
 /* The measured HBM stream-read rate of the device, for the roofline beside
  * the spec peak (SURVEY.md 8(d) "also report a measured stream-read peak"):
- * `reps` launches of a read-only kernel over [d_buf, d_buf + len) (16-byte
- * aligned; a multiple of 16 bytes is read), each timed with hipEvents on
- * `stream`; the best and median launch in microseconds.  Synchronous.
+ * `reps` launches each of three read-only kernels over [d_buf, d_buf + len)
+ * (16-byte aligned; plain loads, nontemporal loads, the scan's LDS-DMA),
+ * each timed with hipEvents on `stream`; the best and median launch of the
+ * fastest form in microseconds.  Synchronous.
  * Diagnostic, not a reference interface. */
 int cdc_debug_stream_read(int device, const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us,
                           void *stream);
