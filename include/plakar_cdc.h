@@ -484,11 +484,11 @@ int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups);
 /* The measured HBM stream-read rate of the device, for the roofline beside
  * the spec peak (SURVEY.md 8(d) "also report a measured stream-read peak"):
  * `reps` launches each of three read-only kernels over [d_buf, d_buf + len)
- * (16-byte aligned; plain loads, nontemporal loads, the scan's LDS-DMA),
- * each timed with hipEvents on `stream`; the best and median launch of the
- * fastest form in microseconds.  Synchronous.
+ * (16-byte aligned), interleaved and timed with hipEvents on `stream`:
+ * best_us[f] / median_us[f] (microseconds) for form f = 0 plain 16-byte
+ * loads, 1 nontemporal loads, 2 the scan's LDS-DMA staging.  Synchronous.
  * Diagnostic, not a reference interface. */
-int cdc_debug_stream_read(int device, const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us,
+int cdc_debug_stream_read(int device, const void *d_buf, uint64_t len, int reps, double best_us[3], double median_us[3],
                           void *stream);
 
 /* Per-chunk digests: the lane count the digest kernels assume the device

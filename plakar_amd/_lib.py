@@ -188,7 +188,7 @@ SIGNATURES = {
                                                       ctypes.c_void_p]),
     "cdc_debug_maskl_state": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_uint32), _P(ctypes.c_uint64)]),
     "cdc_debug_stream_read": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
-                                             _P(ctypes.c_double), _P(ctypes.c_double), ctypes.c_void_p]),
+                                             ctypes.c_double * 3, ctypes.c_double * 3, ctypes.c_void_p]),
     "cdc_debug_set_digest_lanes": (ctypes.c_int, [ctypes.c_uint64]),
     "cdc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cdc_profile_collect": (ctypes.c_int, [_P(ctypes.c_double), _P(ctypes.c_double),

@@ -859,7 +859,7 @@ int cdc_debug_maskl_state(int device, uint32_t *hint, uint64_t *groups)
     return CDC_OK;
 }
 
-int cdc_debug_stream_read(int device, const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us,
+int cdc_debug_stream_read(int device, const void *d_buf, uint64_t len, int reps, double best_us[3], double median_us[3],
                           void *stream)
 {
     if (!d_buf || !best_us || !median_us) return CDC_E_INVALID;

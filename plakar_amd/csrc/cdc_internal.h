@@ -142,7 +142,8 @@ struct ScatterJob {
     const uint8_t *src;
 };
 int launch_gather(const GatherJob *d_jobs, uint32_t n, uint8_t *d_stage, void *stream);
-// k_stream_read over [d_buf, d_buf + len) `reps` times (hipEvents): best and median microseconds.
+// The three stream-read forms over [d_buf, d_buf + len), `reps` launches each (hipEvents): best and
+// median microseconds per form (plain, nontemporal, LDS-DMA) in best_us[3] / median_us[3].
 int launch_stream_read(const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us, void *stream);
 int launch_scatter_digests(const ScatterJob *d_jobs, uint32_t n, void *stream);
 // More than kMaxBufsPerLaunch buffers in ONE launch group: the descriptors go

@@ -2223,6 +2223,7 @@ __global__ __launch_bounds__(kStreamLdsWaves * 64) void k_stream_read_lds(const 
 
 int launch_stream_read(const void *d_buf, uint64_t len, int reps, double *best_us, double *median_us, void *stream)
 {
+    if (!best_us || !median_us) return CDC_E_INVALID;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const uint64_t n16 = len / 16;
     if (n16 == 0 || reps <= 0 || (reinterpret_cast<uintptr_t>(d_buf) & 15u)) return CDC_E_INVALID;
@@ -2235,13 +2236,12 @@ int launch_stream_read(const void *d_buf, uint64_t len, int reps, double *best_u
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipMalloc(&sink, wgs * 4) != hipSuccess) return CDC_E_DEVICE;
     int rc = CDC_OK;
-    std::vector<float> ms;
+    std::vector<float> ms, ms2, ms3;  // per form
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
         hipMemsetAsync(sink, 0, wgs * 4, st) != hipSuccess) {
         rc = CDC_E_DEVICE;
     } else {
-        // the three forms, interleaved; the fastest one's launches are reported
-        std::vector<float> ms2, ms3;
+        // the three forms interleaved, so they see the same clock
         for (int r = 0; r < reps && rc == CDC_OK; ++r) {
             for (int v = 0; v < 3 && rc == CDC_OK; ++v) {
                 float t = 0.f;
@@ -2263,19 +2263,18 @@ int launch_stream_read(const void *d_buf, uint64_t len, int reps, double *best_u
                     (v == 0 ? ms : v == 1 ? ms2 : ms3).push_back(t);
             }
         }
-        if (rc == CDC_OK) {
-            auto lo = [](const std::vector<float> &m) { return *std::min_element(m.begin(), m.end()); };
-            if (lo(ms2) < lo(ms)) ms.swap(ms2);
-            if (lo(ms3) < lo(ms)) ms.swap(ms3);
-        }
     }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     (void)hipFree(sink);
     if (rc != CDC_OK) return rc;
-    std::sort(ms.begin(), ms.end());
-    if (best_us) *best_us = 1e3 * double(ms.front());
-    if (median_us) *median_us = 1e3 * double(ms[ms.size() / 2]);
+    std::vector<float> *by[3] = {&ms, &ms2, &ms3};
+    for (int v = 0; v < 3; ++v) {
+        std::vector<float> &m = *by[v];
+        std::sort(m.begin(), m.end());
+        best_us[v] = 1e3 * double(m.front());
+        median_us[v] = 1e3 * double(m[m.size() / 2]);
+    }
     return CDC_OK;
 }
 
