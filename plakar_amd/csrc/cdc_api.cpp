@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cerrno>
 #include <cctype>
 #include <cstdio>
@@ -1147,20 +1148,42 @@ bool hy_host(void *&p, uint64_t &cap, uint64_t need)
     return true;
 }
 
-// The host's share: the longest chunks, as many as balance the two sides.
-// Device: the longest chunk left to it (its chain); host: the bytes given to
-// `threads` cores (the longest one's chain at least) plus the copy over PCIe.
-size_t hybrid_split(const std::vector<uint64_t> &sorted_desc, int threads)
+// One host core's SHA-256 rate, measured once per process (8 MiB through the
+// same sha256() the workers call): the split below depends on it, and it
+// differs between hosts (SHA extensions or not, clock).
+double host_sha_rate()
 {
-    constexpr double kDevPerByte = 2.05e-6 / 64.0, kHostRate = 1.6e9, kPcie = 40e9;
+    static const double rate = [] {
+        std::vector<uint8_t> buf(8u << 20, 0x5a);
+        uint8_t d[32];
+        sha256(buf.data(), 1u << 20, d);  // warm the code and the pages
+        const auto t0 = std::chrono::steady_clock::now();
+        sha256(buf.data(), buf.size(), d);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return s > 0 ? std::max(2e8, std::min(8e9, double(buf.size()) / s)) : 1.6e9;
+    }();
+    return rate;
+}
+
+// The host's share: the longest chunks, as many as balance the two sides.
+// Device: the longest chunk left to it (its chain, ~2.05 us per 64-B block).
+// Host: its chunks come back over PCIe in `parts` pieces while the threads
+// hash the pieces already landed, so its time is the first piece's copy plus
+// the slower of the copy of the rest and the hashing (bytes over `threads`
+// cores, the longest chunk's own chain at least).
+size_t hybrid_split(const std::vector<uint64_t> &sorted_desc, int threads, int parts)
+{
+    constexpr double kDevPerByte = 2.05e-6 / 64.0, kPcie = 40e9;
+    const double rate = host_sha_rate();
     double best = 1e30, bytes = 0;
     size_t k_best = 0;
     const size_t n = std::min<size_t>(sorted_desc.size(), 1u << 16);
     for (size_t k = 0; k <= n; ++k) {
         const double dev = k < sorted_desc.size() ? double(sorted_desc[k]) * kDevPerByte : 0.0;
-        const double host = k ? std::max(double(sorted_desc[0]) / kHostRate, bytes / (threads * kHostRate)) +
-                                    bytes / kPcie
-                              : 0.0;
+        const double host =
+            k ? bytes / double(std::min<size_t>(size_t(parts), k)) / kPcie +
+                    std::max({double(sorted_desc[0]) / rate, bytes / (threads * rate), bytes / kPcie})
+              : 0.0;
         const double t = std::max(dev, host);
         if (t < best) {
             best = t;
@@ -1243,7 +1266,7 @@ int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64
     } else {
         std::vector<uint64_t> sd(total);
         for (uint64_t q = 0; q < total; ++q) sd[q] = L[order[q]];
-        k = hybrid_split(sd, host_threads);
+        k = hybrid_split(sd, host_threads, 4);
     }
     while (k > 0 && L[order[k - 1]] == 0) --k;  // empty chunks stay on the device
     if (k == 0)
