@@ -166,7 +166,7 @@ def stream_read_peak(torch, L, bufs, dev, local, reps=20):
         return dict(error=int(st))
     names = ("k_stream_read (grid-stride, four plain 16-B loads in flight per lane)",
              "k_stream_read_nt (8-KiB pieces per wave, eight nontemporal 16-B loads per lane)",
-             "k_stream_read_lds (the scan's LDS-DMA: 4-KiB steps per wave into a two-slot ring, nothing computed)")
+             "k_stream_read_lds (the scan's LDS-DMA with its nt policy: 4-KiB steps per wave into a two-slot ring, nothing computed)")
     forms = {nm.split()[0]: dict(best_GBps=round(n / (b * 1e-6) / 1e9, 1), median_GBps=round(n / (m * 1e-6) / 1e9, 1),
                                  form=nm) for nm, b, m in zip(names, best, med)}
     top = max(forms.values(), key=lambda f: f["best_GBps"])

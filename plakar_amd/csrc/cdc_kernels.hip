@@ -321,7 +321,16 @@ __device__ __forceinline__ void wait_vmcnt()
 // One stage's kL LDS-DMA pieces in ONE asm statement: M0 is written and read
 // inside it (and restored), every VGPR offset is read before the statement
 // ends (trailing s_nop guards the compiler's next write of those registers).
+// The staging loads are nontemporal (nt): the bytes are read once.  Measured
+// (tools/ubench_pattern.hip, profiles/r05_scan_dma_nt_ab.txt): LDS-DMA of the
+// scan's pattern reads 7.09 TB/s with nt against 6.20 without; the scan itself
+// +4 % warm, +2 % under the driver's command.  CDC_SCAN_DMA_DEFAULT_POLICY
+// builds the default-policy form (A/B only).
+#ifdef CDC_SCAN_DMA_DEFAULT_POLICY
 #define DMA_PIECE(i) "global_load_lds_dwordx4 %" #i ", %[base]\n\t"
+#else
+#define DMA_PIECE(i) "global_load_lds_dwordx4 %" #i ", %[base] nt\n\t"
+#endif
 #define DMA_NEXT "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
 __device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, const uint32_t (&off)[kL])
 {
