@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 constexpr uint32_t kWaves = 8;    // per workgroup (LDS-DMA: 4 KiB slot x 2 per wave)
@@ -30,6 +31,44 @@ __device__ __forceinline__ uint64_t piece_off(uint64_t wave_base, uint32_t step,
     } else {
         return wave_base + 4096ull * step + 1024u * j + 16u * lane;
     }
+}
+
+#define DMA_ASM(POL)                                                                                        \
+    asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"                        \
+                 "global_load_lds_dwordx4 %1, %[base]" POL "\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"            \
+                 "global_load_lds_dwordx4 %2, %[base]" POL "\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"            \
+                 "global_load_lds_dwordx4 %3, %[base]" POL "\n\ts_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"            \
+                 "global_load_lds_dwordx4 %4, %[base]" POL "\n\t"                                                   \
+                 "s_mov_b32 m0, %[keep]\n\ts_nop 1"                                                               \
+                 : [keep] "=&s"(keep)                                                                              \
+                 : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), [base] "s"(p), [dst] "s"(dst)               \
+                 : "memory", "scc")
+
+// kPol: 0 default, 1 nt, 2 nt sc1, 3 sc0 sc1 nt, 4 sc1
+template <bool kStrided, int kPol = 0>
+__global__ __launch_bounds__(kWaves * 64) void k_dma2(const uint8_t *p, uint64_t steps, uint64_t wave_bytes, uint32_t *sink)
+{
+    __shared__ __attribute__((aligned(16))) char lds[kWaves * 2 * 4096];
+    const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t w = uint64_t(blockIdx.x) * kWaves + wave;
+    const uint64_t wb = w * wave_bytes;
+    const uint32_t slot = uint32_t(reinterpret_cast<uintptr_t>(lds)) + wave * 8192u;
+    for (uint32_t st = 0; st < steps; ++st) {
+        uint32_t keep;
+        const uint32_t dst = slot + (st & 1u) * 4096u;
+        uint32_t off[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) off[j] = uint32_t(piece_off<kStrided>(0, st, j, lane) + wb);
+        if constexpr (kPol == 0) DMA_ASM("");
+        else if constexpr (kPol == 1) DMA_ASM(" nt");
+        else if constexpr (kPol == 2) DMA_ASM(" sc1 nt");
+        else if constexpr (kPol == 3) DMA_ASM(" sc0 sc1 nt");
+        else DMA_ASM(" sc1");
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) sink[blockIdx.x] = *reinterpret_cast<const uint32_t *>(lds);
 }
 
 template <bool kStrided, bool kNt = false>
@@ -135,6 +174,16 @@ int main()
     (void)hipMemset(d, 1, waves * wave_bytes + 4096);
     printf("%d CUs, %llu waves, %.2f GiB read per launch, run %llu B\n", cus, (unsigned long long)waves,
            bytes_strided / double(1ull << 30), (unsigned long long)kRun);
+    if (getenv("UB_POLICIES")) {
+        for (int rep = 0; rep < 2; ++rep) {
+            run("LDS-DMA strided default", k_dma2<true, 0>, wgs, d, steps, wave_bytes, sink, bytes_strided);
+            run("LDS-DMA strided nt", k_dma2<true, 1>, wgs, d, steps, wave_bytes, sink, bytes_strided);
+            run("LDS-DMA strided sc1 nt", k_dma2<true, 2>, wgs, d, steps, wave_bytes, sink, bytes_strided);
+            run("LDS-DMA strided sc0 sc1 nt", k_dma2<true, 3>, wgs, d, steps, wave_bytes, sink, bytes_strided);
+            run("LDS-DMA strided sc1", k_dma2<true, 4>, wgs, d, steps, wave_bytes, sink, bytes_strided);
+        }
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         run("LDS-DMA   strided 8x128 B", k_dma<true>, wgs, d, steps, wave_bytes, sink, bytes_strided);
         run("LDS-DMA   contiguous 1 KiB", k_dma<false>, wgs, d, steps, wave_bytes, sink, bytes_strided);
