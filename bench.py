@@ -1041,22 +1041,45 @@ def main():
                                           f"chunks against {SHA_LANES} resident lanes")
             readers = max(1, args.backup_readers)
             core = host_sha256_rate(L)
-            stage_s = bs["objhash_s"] / readers
             wall = bs["wall_s"]
-            stages = {"object SHA-256 (readers)": stage_s, "reads (readers)": bs["read_s"] / readers,
+            # Per-thread time of each overlapped stage; the longest one names
+            # the steady state.  What sets the wall is that stage between the
+            # pipeline's fill (until batch 0's reads land) and drain (after the
+            # last batch's device stages), or -- for multi-GiB files -- the
+            # longest serial object hash (one file's pieces hash in sequence).
+            stages = {"object SHA-256 (readers)": bs["objhash_s"] / readers, "reads (readers)": bs["read_s"] / readers,
                       "device (calling thread)": bs["device_s"], "packers": bs["pack_s"] / max(1, args.backup_packers)}
             bound_stage = max(stages, key=stages.get)
-            ach = bs["bytes"] / stage_s / 1e9
+            stage_s = stages[bound_stage]
+            fill, drain, chain = bs.get("fill_s", 0.0), bs.get("drain_s", 0.0), bs.get("chain_s", 0.0)
+            pipeline_s = fill + stage_s + drain
+            if chain >= pipeline_s:
+                bound, named_s = "host-sha256 serial chain (the largest file's object hash)", chain
+            else:
+                bound, named_s = f"{bound_stage} between fill and drain", pipeline_s
+            sha_s = bs["objhash_s"] / readers
+            ach = bs["bytes"] / sha_s / 1e9 if sha_s > 0 else None
+            kinds = {"object SHA-256 (readers)": "host-sha256", "reads (readers)": "host-reads",
+                     "device (calling thread)": "device", "packers": "host-packers"}
             line["roofline"] = dict(
-                bound="host-sha256", kernel="object SHA-256 on the reader threads (cdc_sha256, x86 SHA extensions; "
-                                            "objectHasher, snapshot/backup.go:583, 604)",
-                achieved=round(ach, 2), peak=round(readers * core, 2), unit="GB/s",
-                frac=round(ach / (readers * core), 4), traffic=None,
-                per_core_GBps=round(core, 3), readers=readers, stage_s=round(stage_s, 4), wall_s=round(wall, 4),
-                stage_over_wall=round(stage_s / wall, 3), device_busy_frac=round(bs["device_s"] / wall, 3),
-                stage_split_s={k: round(v, 4) for k, v in stages.items()}, longest_stage=bound_stage,
-                note="achieved = bytes / (summed object-hash thread time / readers); peak = readers x one core's "
-                     "SHA-NI rate; the stage that takes longest per thread sets the wall (stage_over_wall); "
+                bound=kinds[bound_stage] if chain < pipeline_s else "host-sha256-chain",
+                wall_set_by=bound, named_s=round(named_s, 4), named_over_wall=round(named_s / wall, 3) if wall else None,
+                wall_s=round(wall, 4), fill_s=round(fill, 4), drain_s=round(drain, 4),
+                longest_stage=bound_stage, longest_stage_s=round(stage_s, 4),
+                stage_over_wall=round(stage_s / wall, 3) if wall else None,
+                chain_s=round(chain, 4), chain_bytes=bs.get("chain_bytes", 0),
+                chain_over_wall=round(chain / wall, 3) if wall else None,
+                chain_GBps=round(bs.get("chain_bytes", 0) / chain / 1e9, 3) if chain > 0 else None,
+                kernel="object SHA-256 on the reader threads (cdc_sha256, x86 SHA extensions; "
+                       "objectHasher, snapshot/backup.go:583, 604)",
+                achieved=round(ach, 2) if ach else None, peak=round(readers * core, 2), unit="GB/s",
+                frac=round(ach / (readers * core), 4) if ach else None, traffic=None,
+                per_core_GBps=round(core, 3), readers=readers,
+                device_busy_frac=round(bs["device_s"] / wall, 3) if wall else None,
+                stage_split_s={k: round(v, 4) for k, v in stages.items()},
+                note="named_s = what sets the wall: fill + the longest per-thread stage + drain, or the longest "
+                     "serial object SHA-256 chain when that is longer; achieved / peak = the readers' object "
+                     "hashing (bytes / (summed hash time / readers)) against readers x one core's SHA-NI rate; "
                      "device_busy_frac = the calling thread's device time / wall",
                 device_kernel=device_kernel, scan=roofline)
             line["backup_stages"] = dict(

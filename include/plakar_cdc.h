@@ -290,6 +290,13 @@ typedef struct cdc_backup_stats {
      * share queues with them even at 8. */
     int32_t hw_queues;
     int32_t streams_serialised;  /* 1 when hw_queues < 8 (or unset) */
+    /* What sets the wall (round 6): fill_s, the call's start until batch 0's
+     * reads have landed (the device's first work); drain_s, the last batch's
+     * device stages done until the call returns (Encode, packers, callbacks
+     * of the tail); chain_s / chain_bytes, the longest serial object SHA-256
+     * chain of one file (a file's pieces hash one after another). */
+    double fill_s, drain_s, chain_s;
+    uint64_t chain_bytes;
 } cdc_backup_stats;
 typedef void (*cdc_backup_file_fn)(void *ctx, const cdc_backup_file *f);
 typedef int (*cdc_backup_pack_fn)(void *ctx, const uint8_t *packfile, uint64_t len);
@@ -467,14 +474,6 @@ int cdc_set_debug_mode(int mode);
  * reference interface (the Go chunker has no index).  Returns CDC_OK or
  * CDC_E_INVALID. */
 int cdc_set_maskl_index_mode(int mode);
-
-/* How a launch group resolves its cut points: 0 = by a second launch after
- * the scan (k_scan + k_resolve, the default), 1 = in the same launch as the
- * scan (k_chunk / k_chunk_f, where the MaskL index does not need k_scan_l;
- * measured slower).  Cut points never depend on it; the GPU
- * tests run both.  Initial value from the CDC_RESOLVE_MODE environment
- * variable.  Not a reference interface.  Returns CDC_OK or CDC_E_INVALID. */
-int cdc_set_resolve_mode(int mode);
 
 /* Adaptive MaskL state of one device (diagnostics, after a device sync):
  * *hint = 1 while the next launch groups build the MaskL index (a recent

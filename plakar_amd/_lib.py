@@ -72,7 +72,8 @@ class cdc_backup_stats(ctypes.Structure):
                [(n, ctypes.c_double) for n in ("read_s", "objhash_s", "h2d_s", "chunk_s", "digest_s", "d2h_s",
                                                "encode_s", "device_s", "callback_s", "read_wait_s", "pack_s", "wall_s")] + \
                [(n, ctypes.c_uint64) for n in ("failed_files", "pieces", "slot_arena_bytes")] + \
-               [("hw_queues", ctypes.c_int32), ("streams_serialised", ctypes.c_int32)]
+               [("hw_queues", ctypes.c_int32), ("streams_serialised", ctypes.c_int32)] + \
+               [(n, ctypes.c_double) for n in ("fill_s", "drain_s", "chain_s")] + [("chain_bytes", ctypes.c_uint64)]
 
 
 BACKUP_FILE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(cdc_backup_file))
@@ -175,7 +176,6 @@ SIGNATURES = {
     "cdc_set_debug_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_gear_is_placeholder": (ctypes.c_int, []),
     "cdc_set_maskl_index_mode": (ctypes.c_int, [ctypes.c_int]),
-    "cdc_set_resolve_mode": (ctypes.c_int, [ctypes.c_int]),
     "cdc_backup_run": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_char_p), ctypes.c_int, _P(cdc_backup_opts),
                                       BACKUP_FILE_FN, BACKUP_PACK_FN, ctypes.c_void_p, _P(cdc_backup_stats)]),
     "cdc_backup_new": (ctypes.c_int, [ctypes.c_int, _P(cdc_backup_opts), _P(ctypes.c_void_p)]),

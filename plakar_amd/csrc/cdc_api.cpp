@@ -90,21 +90,6 @@ Global &G()
     return g;
 }
 
-// Resolution mode (cdc_set_resolve_mode; initial value from CDC_RESOLVE_MODE):
-// 0 two launches (k_scan + k_resolve, the default), 1 the scan and the
-// resolution in one launch (k_chunk / k_chunk_f) wherever the MaskL index
-// does not need k_scan_l.  One launch measured slower (DESIGN.md 5.3,
-// profiles/r05_one_launch_ab.txt): its resolution waves, at 168 VGPRs with
-// spills, slow the last scan tasks.
-std::atomic<uint32_t> &resolve_mode()
-{
-    static std::atomic<uint32_t> m([] {
-        const char *e = getenv("CDC_RESOLVE_MODE");
-        return e && e[0] == '1' ? 1u : 0u;
-    }());
-    return m;
-}
-
 // MaskL index mode (cdc_set_maskl_index_mode; initial value from CDC_MASKL_INDEX)
 std::atomic<uint32_t> &maskl_index_mode()
 {
@@ -271,7 +256,6 @@ Workspace carve(void *ws, const Plan &pl, const uint64_t *gear)
     W.sg = reinterpret_cast<uint64_t *>(b + pl.off_sg);
     W.flags = reinterpret_cast<uint32_t *>(b + pl.off_flags);
     W.tick = reinterpret_cast<uint32_t *>(b + pl.off_tick);
-    W.tdone = reinterpret_cast<uint32_t *>(b + pl.off_tdone);
     W.gear = gear;
     W.runsL = reinterpret_cast<uint64_t *>(b + pl.off_runsL);
     W.validL = reinterpret_cast<uint32_t *>(b + pl.off_validL);
@@ -302,6 +286,10 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         return e ? uint32_t(atoi(e)) : 0u;
     }();
     B.debug = dbg;
+    if (G().debug_mode == 2 || t_force_abort) {  // the device-abort path: a wait that never ends, a short spin limit
+        B.debug |= kDbgForceAbort;
+        B.spin_ticks = kForceAbortTicks;
+    }
     // MaskL index.  CDC_MASKL_INDEX / cdc_set_maskl_index_mode: 0 off (walkers
     // raw-scan every MaskL region), 1 adaptive (default), 2 every group (in the
     // MaskS pass, k_scan_f, where the masks admit it), 3 every group by
@@ -323,8 +311,6 @@ int run_group(DeviceCtx *ctx, const DevParams &P, const void *const *data, const
         B.maskl_hint = ctx->hint_d;
     }
     B.force_fallback = G().debug_mode == 1 ? 1u : 0u;
-    // one launch (k_chunk / k_chunk_f) unless the MaskL index needs k_scan_l
-    B.one_launch = resolve_mode().load(std::memory_order_relaxed) == 1 && (!B.maskl_index || B.maskl_fused) ? 1u : 0u;
     uint32_t segs = 0, tasks = 0;
     for (int i = 0; i < n; ++i) {
         BufDesc &D = B.b[i];
@@ -823,13 +809,6 @@ int cdc_set_debug_mode(int mode)
     return CDC_OK;
 }
 
-int cdc_set_resolve_mode(int mode)
-{
-    if (mode < 0 || mode > 1) return CDC_E_INVALID;
-    resolve_mode().store(uint32_t(mode), std::memory_order_relaxed);
-    return CDC_OK;
-}
-
 int cdc_set_maskl_index_mode(int mode)
 {
     if (mode < 0 || mode > 3) return CDC_E_INVALID;
@@ -1292,6 +1271,17 @@ int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64
     GatherJob *hgj = static_cast<GatherJob *>(H.h_gj), *dgj = static_cast<GatherJob *>(H.d_gj);
     ScatterJob *hsj = static_cast<ScatterJob *>(H.h_sj), *dsj = static_cast<ScatterJob *>(H.d_sj);
     uint8_t *hdig = static_cast<uint8_t *>(H.h_dig), *ddig = static_cast<uint8_t *>(H.d_dig);
+    // From the first enqueue on, every return drains both streams: copies out
+    // of the scratch buffers (and gathers from the caller's data) must not
+    // outlive this call, whose scratch the next call may free or reuse.
+    struct Drain {
+        hipStream_t a, b;
+        ~Drain()
+        {
+            (void)hipStreamSynchronize(a);
+            (void)hipStreamSynchronize(b);
+        }
+    } drain{H.side, sm};
     // the copy from pageable memory completes before hipMemcpyAsync returns
     if (hipMemcpyAsync(dcuts, mod.data(), total * sizeof(cdc_cut), hipMemcpyHostToDevice, sm) != hipSuccess)
         return CDC_E_DEVICE;
@@ -1373,10 +1363,7 @@ int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64
     }
     worker();
     for (auto &t : ts) t.join();
-    if (fail.load() != CDC_OK) {
-        (void)hipStreamSynchronize(H.side);
-        return fail.load();
-    }
+    if (fail.load() != CDC_OK) return fail.load();
     // the host's digests into their rows, after the device's digest kernel
     if (hipStreamWaitEvent(H.side, H.ev_dig, 0) != hipSuccess ||
         hipMemcpyAsync(ddig, hdig, 32 * k, hipMemcpyHostToDevice, H.side) != hipSuccess ||

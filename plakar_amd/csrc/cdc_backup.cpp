@@ -129,6 +129,7 @@ struct FileState {
     uint8_t obj[32] = {};         // the object checksum
     double ent_acc = 0.0;         // Object.Entropy's running sum (callback thread)
     bool ent_any = false;
+    double chain_s = 0.0;         // its object hash so far (the pieces hash in sequence)
 };
 
 struct Batch {
@@ -330,6 +331,8 @@ struct Run {
     std::set<uint32_t> hash_q;     // units read, not yet hashed, in unit order (guarded by mu)
     std::set<uint32_t> prefix_q;   // pieces j > 0 whose [nb, ne) is read, not yet their carried prefix (mu)
     int64_t fail_file = -1, fail_piece = -1;  // CDC_BACKUP_FAIL_PIECE=file:piece (test hook): that read fails
+    int64_t fail_dev_file = -1, fail_dev_piece = -1;  // CDC_BACKUP_FAIL_DEVICE=file:piece: its launch aborts (debug mode 2)
+    double last_dev_end = 0.0;  // seconds into the call when the last batch's device stages were done
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<int> status{CDC_OK};
@@ -373,6 +376,13 @@ struct Run {
             if (std::sscanf(f, "%ld:%ld", &a, &c) == 2) {
                 fail_file = a;
                 fail_piece = c;
+            }
+        }
+        if (const char *f = std::getenv("CDC_BACKUP_FAIL_DEVICE")) {
+            long a = -1, c = -1;
+            if (std::sscanf(f, "%ld:%ld", &a, &c) == 2) {
+                fail_dev_file = a;
+                fail_dev_piece = c;
             }
         }
     }
@@ -556,6 +566,9 @@ void reader_main(Run &R)
                 Unit &u = R.units[i];
                 FileState &F = R.files[u.file];
                 if (u.err == CDC_OK && F.err != CDC_OK) u.err = F.err;  // an earlier piece failed
+                // the carry is the previous piece's undecided tail: fewer than
+                // Max bytes before nb (anything else is a device failure)
+                if (u.err == CDC_OK && !(F.next_start <= u.nb && F.next_start + M > u.nb)) u.err = CDC_E_DEVICE;
                 u.start = u.err == CDC_OK ? F.next_start : u.nb;
                 u.len = u.err == CDC_OK ? u.ne - u.start : 0;
                 u.data_off = fixed_off(u, M) - (u.nb - u.start);
@@ -636,10 +649,12 @@ void reader_main(Run &R)
                 if (u.piece + 1 == u.pieces) F.sha.final(F.obj);
             }
         }
-        hash_s += secs(t1, Clock::now());
+        const double dt = secs(t1, Clock::now());
+        hash_s += dt;
         R.ev("hash_end", k, i, u.len);
         {
             std::lock_guard<std::mutex> lk(R.mu);
+            F.chain_s += dt;
             if (u.pieces > 1) F.hashed_pieces = u.piece + 1;
             if (++s.nhashed == b.u1 - b.u0) {
                 s.hash_done = true;
@@ -780,13 +795,19 @@ int enqueue_cuts(Run &R, size_t k)
     // inside the piece, and the rest is carried into the next piece
     const Unit &u0 = R.units[b.u0];
     const int final_ = u0.piece + 1 < u0.pieces ? 0 : 1;
+    // test hook: this piece's launch group takes the forced device abort
+    cdc::t_force_abort = R.fail_dev_file == int64_t(u0.file) && R.fail_dev_piece == int64_t(u0.piece) ? 1 : 0;
     for (uint32_t g = 0; g < nf; g += cdc::kMaxBufsPerLaunch) {
         const int m = int(std::min<uint32_t>(cdc::kMaxBufsPerLaunch, nf - g));
         const int st = cdc_chunk_device_batch_async(R.B->device, dp.data() + g, s.lens.data() + g, m, final_, co,
                                                     cp.data() + g, caps.data() + g, rp.data() + g, s.d_ws, s.ws_cap,
                                                     st1);
-        if (st != CDC_OK) return st;
+        if (st != CDC_OK) {
+            cdc::t_force_abort = 0;
+            return st;
+        }
     }
+    cdc::t_force_abort = 0;
     HIPOK(hipEventRecord(s.ev[2], st1));
     s.t_enq = secs(w0, Clock::now());
     return CDC_OK;
@@ -853,6 +874,7 @@ int finish_device(Run &R, size_t k)
             if (hipEventElapsedTime(&ms, R.trace_ref, s.ev[e]) == hipSuccess) R.ev(kDevEv[e], int64_t(k), -1, 0, ms * 1e-3);
         }
     }
+    int piece_err = CDC_OK;
     {  // a non-final piece: publish where the next piece starts (its reader waits for it)
         const Unit &u = R.units[b.u0];
         if (u.piece + 1 < u.pieces) {
@@ -861,12 +883,17 @@ int finish_device(Run &R, size_t k)
             if (u.err == CDC_OK && s.h_res[0].status == CDC_OK) {
                 F.next_start = u.start + s.h_res[0].consumed;
                 // a piece of P >> Max bytes always emits a chunk; the carry is < Max
-                if (F.next_start <= u.start || u.ne - F.next_start >= R.o.chunking.max_size) return CDC_E_DEVICE;
+                if (F.next_start <= u.start || u.ne - F.next_start >= R.o.chunking.max_size) piece_err = CDC_E_DEVICE;
+            } else if (u.err == CDC_OK) {  // the device row failed: no carry to publish
+                piece_err = s.h_res[0].status < 0 ? int(s.h_res[0].status) : CDC_E_DEVICE;
             }
+            // the next piece's reader sees the failure before it takes a prefix
+            if (piece_err != CDC_OK && F.err == CDC_OK) F.err = piece_err;
             F.dev_pieces = u.piece + 1;
         }
     }
     R.cv.notify_all();
+    if (piece_err != CDC_OK) return piece_err;
     float t[4] = {};  // H2D, cut points, digests + entropy, lists back
     HIPOK(hipEventElapsedTime(&t[0], s.ev[0], s.ev[1]));
     HIPOK(hipEventElapsedTime(&t[1], s.ev[1], s.ev[2]));
@@ -1286,7 +1313,9 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
             for (size_t k = 0; k < nb && st == CDC_OK; ++k) {
                 if (R.digs == k) {
                     if (R.cuts == k) {
-                        if ((st = wait_read(R, k)) != CDC_OK || (st = enqueue_cuts(R, k)) != CDC_OK) break;
+                        if ((st = wait_read(R, k)) != CDC_OK) break;
+                        if (k == 0) R.st.fill_s = secs(w0, Clock::now());
+                        if ((st = enqueue_cuts(R, k)) != CDC_OK) break;
                         ++R.cuts;
                     }
                     if ((st = enqueue_digests(R, k)) != CDC_OK) break;
@@ -1294,6 +1323,7 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
                 }
                 if ((st = pump(R, k)) != CDC_OK) break;
                 if ((st = finish_device(R, k)) != CDC_OK) break;
+                R.last_dev_end = secs(w0, Clock::now());
                 {
                     std::lock_guard<std::mutex> lk(R.mu);
                     R.devices_done = k + 1;
@@ -1341,6 +1371,12 @@ int cdc_backup_files(cdc_backup *B, const char *const *paths, int n, cdc_backup_
         for (auto &sm : B->stream) (void)hipStreamSynchronize(sm);
     }
     R.st.wall_s = secs(w0, Clock::now());
+    R.st.drain_s = R.last_dev_end > 0 ? R.st.wall_s - R.last_dev_end : 0.0;
+    for (const FileState &F : R.files)
+        if (F.chain_s > R.st.chain_s) {
+            R.st.chain_s = F.chain_s;
+            R.st.chain_bytes = F.size;
+        }
     R.ev("end", -1);
     if (R.trace_path) {
         if (FILE *f = std::fopen(R.trace_path, "w")) {

@@ -601,6 +601,7 @@ int launch_arena_cuts(const uint64_t *d_meta, uint32_t nfiles, const cdc_result 
 
 uint64_t g_digest_lanes = 0;  // cdc_debug_set_digest_lanes (0: from the device's CU count)
 thread_local int t_scan_tpw = -1;
+thread_local int t_force_abort = 0;
 
 namespace {
 

@@ -12,6 +12,14 @@
 namespace cdc {
 
 constexpr int kMaxBufsPerLaunch = 32;   // buffers per launch group (kernel-arg budget)
+// A result row's status between the scan kernel and k_resolve's last segment
+// (never returned: the last segment or an aborting wave overwrites it).
+constexpr int64_t kRowPending = -0x7FF0;
+// Batch.debug bit of debug mode 2 (cdc_set_debug_mode): segment 0 of buffer 0
+// never publishes its speculative exit, so segment 1's bounded wait gives up
+// and the launch aborts (the device-abort path under test).
+constexpr uint32_t kDbgForceAbort = 512;
+constexpr uint32_t kForceAbortTicks = 20000;  // that mode's spin limit: 200 us
 // Candidate index: one u64 record per scan-lane run (scan_lane bytes of one
 // buffer): bits 0-7 the number of full-window MaskS candidates in the run
 // (saturating), bits 8-63 the first kRunCap of them as 14-bit offsets from the
@@ -66,13 +74,13 @@ struct Batch {
     uint32_t force_fallback; // debug: resolve with the sequential single-wave walker
     uint32_t scan_lane;      // bytes per scan lane (= per index run); one wave (scan task) = 64 lanes
     uint32_t debug;          // profiling experiments (CDC_DEBUG_PHASE); 0 in production
+    uint32_t spin_ticks;     // bounded waits give up after this many 100-MHz ticks (0: 2 s; debug mode 2: short)
     uint32_t maskl_index;    // 1: k_scan_l builds the MaskL index of long MaskS-free stretches (walkers use it)
     uint32_t maskl_fused;    // 1 (with maskl_index): k_scan_f builds both indexes of every task in one pass
     uint32_t *maskl_hint;    // mapped host word: set when some task needed the MaskL index
     uint32_t maskl_probe;    // 1: k_maskl_probe runs the selection test (adaptive mode, hint not set)
     uint64_t seg;            // resolution segment length in bytes
     uint32_t persist;        // 1: k_scan / k_scan_f run scan_wgs persistent workgroups pulling tasks
-    uint32_t one_launch;     // 1: k_chunk, the scan and the resolution in ONE launch (no MaskL index)
     uint32_t scan_wgs;
     BufDesc b[kMaxBufsPerLaunch];
 };
@@ -86,12 +94,7 @@ struct Workspace {
     uint64_t *xg;        // [total_segs] granule: published | node count | speculative exit X_q
     uint64_t *sg;        // [total_segs] granule: LOCAL (conv, cuts) or INCLUSIVE (E, O)
     uint32_t *flags;     // [kMaxBufsPerLaunch + 4] per-buffer "resolve sequentially", then the abort word
-    uint32_t *tick;      // [16 + tasks] [0] segment ticket, [2] persistent scan task counter, [8..16) k_chunk "tasks
-                         // taken" shards, [16..) k_chunk per-task claims
-    // k_chunk: per scan task, 1 once its run records are stored (write-through)
-    // and readable by another workgroup.  xg .. tdone is one contiguous range,
-    // zeroed before every k_chunk launch.
-    uint32_t *tdone;     // [total_tasks]
+    uint32_t *tick;      // [16] [0] segment ticket, [2] persistent scan task counter
     const uint64_t *gear;  // 256 entries, device copy
     // MaskL candidate index (same record format as runs), built by k_scan_l
     // only for the scan tasks near a long MaskS-free stretch; validL[task]
@@ -105,7 +108,7 @@ struct Plan {
     uint32_t scan_lane;
     uint32_t total_segs, total_tasks;
     uint32_t persist, scan_wgs;
-    size_t off_runs, off_w1_nodes, off_xg, off_sg, off_flags, off_tick, off_tdone, off_runsL, off_validL,
+    size_t off_runs, off_w1_nodes, off_xg, off_sg, off_flags, off_tick, off_runsL, off_validL,
         bytes;
 };
 
@@ -160,6 +163,9 @@ extern uint64_t g_digest_lanes;
 extern thread_local int t_scan_tpw;
 // The calling thread's Encode workspace (0 or 1) for cdc_encode_device.
 extern thread_local int t_encode_ws;
+// Test hook (the backup's CDC_BACKUP_FAIL_DEVICE): the calling thread's next
+// launch groups run in debug mode 2 (the forced device abort) while nonzero.
+extern thread_local int t_force_abort;
 
 // cdc_api.cpp: a host-buffer pipeline on one device that outlives one call
 // (the collector's per-device worker).  The source hands out batches of at

@@ -223,11 +223,8 @@ constexpr uint32_t kClkRecs = 4096;
 constexpr uint32_t kTsClkN = kTsClk + 4 * kClkRecs;   // ring counter
 constexpr uint32_t kTsHw = kTsClkN + 1;               // per scan workgroup: XCC_ID << 32 | HW_ID (kDbgTs)
 constexpr uint32_t kTsAbort = kTsHw + 4096;           // the last wait that gave up: kind, two values, time
-constexpr uint32_t kTsTask = kTsAbort + 4;            // k_chunk (kDbgTs): per scan task start, end, wave, XCC << 32 | HW_ID
-constexpr uint32_t kTsTasks = 8192;
-constexpr uint32_t kTsSlots = kTsTask + 4 * kTsTasks;
+constexpr uint32_t kTsSlots = kTsAbort + 4;
 constexpr uint32_t kDbgClk = 64;
-constexpr uint32_t kDbgScanOnly = 256;  // k_chunk: waves exit after the scan (no cut lists; timing / hang probes)
 __device__ uint64_t g_ts[kTsSlots];
 
 __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v = ~0ull)
@@ -235,28 +232,34 @@ __device__ __forceinline__ void dbg_ts(const Batch &B, uint32_t slot, uint64_t v
     if ((B.debug & kDbgTs) && slot < kTsSlots) g_ts[slot] = v == ~0ull ? __builtin_amdgcn_s_memrealtime() : v;
 }
 
-// Bounded waits.  Every spin of a walker (task flags, granules, look-back
-// statuses) gives up after kSpinLimit of its own waiting (s_memrealtime,
-// 100 MHz) or as soon as another wait of the launch gave up: it raises the
-// launch's abort word (W.flags[kAbortWord]), records what it waited for at
-// g_ts[kTsAbort], and the launch's result rows report CDC_E_DEVICE instead
-// of the device hanging.  No correct launch waits that long.
+// Bounded waits.  Every spin of a walker (granules, look-back statuses)
+// gives up after the launch's spin limit of its own waiting (s_memrealtime,
+// 100 MHz; W.flags[kLimitWord], written by the scan kernel: 2 s, or B.spin_ticks
+// in the forced-abort debug mode) or as soon as another wait of the launch
+// gave up.  It raises the launch's abort word (W.flags[kAbortWord]) and
+// records what it waited for at g_ts[kTsAbort]; the wave then publishes an
+// ABORTED status (look-back propagates it) and stores CDC_E_DEVICE into every
+// result row of the launch group, so the caller gets an error instead of a
+// hung device.  No correct launch waits that long.
 constexpr uint32_t kAbortWord = kMaxBufsPerLaunch;
-constexpr uint64_t kSpinLimit = 200000000ull;  // 2 s
-enum : uint32_t { kWaitTask = 1, kWaitJunction, kWaitPrev, kWaitLook, kWaitLookSlow, kWaitLast };
+constexpr uint32_t kLimitWord = kMaxBufsPerLaunch + 1;  // spin limit, in 100-MHz ticks (>= 1)
+constexpr uint64_t kSpinLimit = 200000000ull;            // 2 s
+enum : uint32_t { kWaitJunction = 2, kWaitPrev, kWaitLook, kWaitLookSlow, kWaitLast };
 
 struct SpinGuard {
-    uint64_t t0 = 0;
+    uint64_t t0 = 0, lim = 0;
     // true: poll again; false: give up
     __device__ __forceinline__ bool ok(uint32_t *flags, uint32_t kind, uint64_t a, uint64_t b)
     {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (!t0) {
             t0 = now;
+            lim = __hip_atomic_load(flags + kLimitWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!lim) lim = kSpinLimit;
             return true;
         }
         if (__hip_atomic_load(flags + kAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-        if (now - t0 < kSpinLimit) return true;
+        if (now - t0 < lim) return true;
         if ((threadIdx.x & 63u) == 0) {
             __hip_atomic_store(flags + kAbortWord, kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             g_ts[kTsAbort] = kind;
@@ -279,11 +282,14 @@ struct SpinGuard {
 // fp bit the masks can see (bits 0..hb) and the high dword of fp' holds the
 // top 32 of them.  The hot test per byte is one v_and of that dword with the
 // shifted MaskS high half (13 of the 15 default MaskS bits): a necessary
-// condition, reduced by v_min3 to one branch per 16 bytes.  A group whose
-// filter fired (2^-13 per byte at the default masks) is re-rolled exactly
-// (all mask bits, and the lane's [s, e) bounds), so warm-up bytes, bytes past
-// the lane's run and lanes past the buffer's end need no separate code path:
-// every stage of every lane runs the same straight-line loop.
+// condition, reduced by v_min3 to one wave-uniform branch per 32 bytes.  A
+// lane whose filter fired (2^-13 per byte at the default masks: some lane of
+// the wave in ~22 % of 32-byte groups) queues the group in LDS, and the queue
+// is re-rolled exactly -- all mask bits, the run's bounds -- one group per
+// lane, at the end of the task (see the recheck queue in scan_task), so
+// warm-up bytes, bytes past the lane's run and lanes past the buffer's end
+// need no separate code path: every stage of every lane runs the same
+// straight-line loop.
 //
 // The next group's 16 Gear gathers are issued byte by byte between the links
 // of the current group's fingerprint chain, into the registers its roll has
@@ -305,7 +311,15 @@ constexpr uint32_t kL = kStage / 16;                  // 16-B pieces per lane pe
 constexpr uint32_t kGroups = kStage / 16;             // 16-byte groups per stage
 constexpr uint32_t kStageBytes = 64u * kStage;        // per wave per stage (one LDS slot)
 constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
-static_assert(kGearLdsBytes + kS2Waves * kStageBytes <= 160u * 1024u, "LDS budget");
+// Recheck queue: 32-byte groups per wave, 12 bytes each (fp before the group;
+// its offset in the run and the lane).  64 items keep the scan workgroup at
+// 121 KiB of LDS, so a k_resolve workgroup (36.3 KiB) of the other stream
+// still fits beside it on a CU (at 128 items of 16 B it did not: pipelined
+// -2 % warm, profiles/r06_*).
+constexpr uint32_t kQCap = 64;
+constexpr uint32_t kQBytes = kQCap * 12u;
+static_assert(kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes) + 37128u <= 160u * 1024u,
+              "LDS budget: a scan workgroup and a k_resolve workgroup per CU");
 // Scan lane lengths are multiples of kLaneQuant (16-B aligned runs: every lane
 // of a buffer has the same stage alignment; 256 B avoided the slow strides
 // seen at odd multiples of 128 B, see make_plan).
@@ -350,12 +364,37 @@ __device__ __forceinline__ void dma_stage(uint64_t base_in, uint32_t dst_in, con
                  : "memory", "scc");
 }
 
+// The same four pieces with M0 set once: piece j carries the instruction
+// offset 1024 j, which LDS-DMA applies to the global AND the LDS address, so
+// the per-lane offsets come with 1024 j already subtracted (offi) and M0 is
+// not stepped between the pieces (3 SALU per stage fewer).
+#ifdef CDC_SCAN_DMA_DEFAULT_POLICY
+#define DMA_PIECE_IMM(i, o) "global_load_lds_dwordx4 %" #i ", %[base] offset:" #o "\n\t"
+#else
+#define DMA_PIECE_IMM(i, o) "global_load_lds_dwordx4 %" #i ", %[base] offset:" #o " nt\n\t"
+#endif
+__device__ __forceinline__ void dma_stage_imm(uint64_t base_in, uint32_t dst_in, const uint32_t (&offi)[kL])
+{
+    static_assert(kL == 4, "four 1-KiB pieces per stage");
+    const uint64_t base = (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(base_in >> 32)))) << 32) |
+                          uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(base_in)));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(dst_in);
+    uint32_t keep;
+    asm volatile("s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[dst]\n\ts_nop 0\n\t"
+                 DMA_PIECE_IMM(1, 0) DMA_PIECE_IMM(2, 1024) DMA_PIECE_IMM(3, 2048) DMA_PIECE_IMM(4, 3072)
+                 "s_mov_b32 m0, %[keep]\n\ts_nop 1"
+                 : [keep] "=&s"(keep)
+                 : "v"(offi[0]), "v"(offi[1]), "v"(offi[2]), "v"(offi[3]), [base] "s"(base), [dst] "s"(dst)
+                 : "memory");
+}
+
 // One ticket per wave from an agent-scope counter.  Every lane takes part in
 // the atomic (lane 0 adds 1, the others 0), so no lane-0 branch precedes the
 // readfirstlane: after such a branch the compiler may thread it into a
-// neighbouring lane-0 branch (k_chunk's flag store before its next claim),
-// and the readfirstlane then runs for lanes 1-63 while lane 0 is still on the
-// other path -- they read 0 and loop on task 0 (measured: a hang).
+// neighbouring lane-0 branch (round 5's one-launch resolver stored a flag
+// there before its next claim), and the readfirstlane then runs for lanes 1-63
+// while lane 0 is still on the other path -- they read 0 and loop on task 0
+// (measured: a hang).
 __device__ __forceinline__ uint32_t wave_ticket(uint32_t *p)
 {
     const uint32_t old = __hip_atomic_fetch_add(p, (threadIdx.x & 63u) == 0u ? 1u : 0u, __ATOMIC_RELAXED,
@@ -376,14 +415,6 @@ __device__ __forceinline__ uint32_t rec_ent(uint64_t rec, uint32_t e)
     return uint32_t(rec >> (kRecCntBits + kRecEntBits * e)) & ((1u << kRecEntBits) - 1);
 }
 
-// A run record: plain for the next launch, or write-through (relaxed agent
-// store, sc1) for walkers of the same launch (k_chunk).
-__device__ __forceinline__ void put_rec(uint64_t *p, uint64_t v, bool wt)
-{
-    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
-
 // Each lane keeps its run's index record in a register (count + the first
 // kRunCap offsets, see cdc_internal.h) and stores it after its last stage:
 // one coalesced 8-byte store per run, no atomics.
@@ -392,32 +423,6 @@ __device__ __forceinline__ void record_hit(uint64_t &rec, int32_t r)
     const uint32_t c = rec_cnt(rec);
     if (c < kRunCap) rec |= uint64_t(uint32_t(r)) << (kRecCntBits + kRecEntBits * c);
     if (c < (1u << kRecCntBits) - 1) ++rec;
-}
-
-// Exact MaskS test of one 16-byte group in the shifted frame, from fp' before
-// the group and the group's 16 Gear values; r0 is the group's first position
-// relative to the lane's run start, whose length is len (positions outside
-// [0, len) are warm-up or past the run and are ignored).  Runs when the
-// hi-dword filter fired in some lane of the wave (2^-13 per byte at the
-// default masks), exec-masked to those lanes.
-__device__ __forceinline__ void recheck_group(uint64_t f, const uint64_t (&g)[16], int32_t r0, int32_t len,
-                                           uint32_t xlo, uint32_t xhi, uint64_t &rec)
-{
-    uint32_t key[16];
-    uint32_t m = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        f = (f << 1) + g[k];
-        key[k] = __builtin_amdgcn_bitop3_b32(uint32_t(f >> 32), xhi, uint32_t(f) & xlo, 0xEA);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) m = umin3(m, key[k], key[k + 1]);
-    if (m != 0) return;  // filter false positive (3 in 4 at the default masks)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int32_t r = r0 + k;
-        if (key[k] == 0 && r >= 0 && r < len) record_hit(rec, r);
-    }
 }
 
 // Does scan task `t` of buffer D (buffer-relative) need the MaskL index?  A
@@ -484,32 +489,7 @@ __device__ bool maskl_needed(const Batch &B, const DevParams &P, const Workspace
     return false;
 }
 
-// Exact MaskL test of one 16-byte group inside the MaskS frame (k_scan_f):
-// the window of fp' from bit ws holds all of MaskL's bits, so the fused
-// filter is exact and this only records the positions.
-__device__ __forceinline__ void record_l_group(uint64_t f, const uint64_t (&g)[16], int32_t r0, int32_t len,
-                                               uint32_t ws, uint32_t m, uint64_t &rec)
-{
-    // the group's hits as a bit mask, then one record per set bit (MaskL
-    // candidates are 2^-11 per byte against MaskS's 2^-15 on random data: 16
-    // exec-masked branches per firing group cost C3 1.4 %)
-    uint32_t miss = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        f = (f << 1) + g[k];
-        miss |= min(__builtin_amdgcn_alignbit(uint32_t(f >> 32), uint32_t(f), ws) & m, 1u) << k;
-    }
-    const int32_t lo = r0 < 0 ? -r0 : 0, hi = len - r0;
-    uint32_t hm = ~miss & 0xFFFFu;
-    hm &= lo >= 16 ? 0u : (0xFFFFu << lo);
-    hm &= hi >= 16 ? 0xFFFFu : (hi <= 0 ? 0u : (1u << hi) - 1u);
-    while (hm) {
-        record_hit(rec, r0 + int32_t(__builtin_ctz(hm)));
-        hm &= hm - 1u;
-    }
-}
-
-template <bool kMaskL, bool kFused, bool kOne = false>
+template <bool kMaskL, bool kFused>
 __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, const Workspace &W, char *s_lds,
                                           const char *tab, uint32_t task, uint32_t lane, uint32_t wave,
                                           uint32_t laneoff);
@@ -521,7 +501,7 @@ template <bool kMaskL, bool kFused = false>
 __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
     static_assert(!(kMaskL && kFused), "k_scan_f builds both indexes in the MaskS frame");
-    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * kStageBytes];
+    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes)];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
@@ -547,8 +527,10 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
             W.xg[i] = 0ull;
             W.sg[i] = 0ull;
         }
-        if (gt < kMaxBufsPerLaunch + 4) W.flags[gt] = 0u;  // + the abort word
+        if (gt < kMaxBufsPerLaunch + 4)  // + the abort word and the spin limit
+            W.flags[gt] = gt == kLimitWord ? uint32_t(B.spin_ticks ? B.spin_ticks : kSpinLimit) : 0u;
         if (gt < 2) W.tick[gt] = 0u;
+        if (gt < B.nbufs) B.b[gt].res->status = kRowPending;  // k_resolve's last segment settles it
         if (threadIdx.x == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x);
     }
     // clock ring: workgroup 0's span in the 100-MHz and the shader-clock counters
@@ -589,9 +571,8 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
 }
 
 // One scan task: the 64 lane runs of task `task` (64 * B.scan_lane bytes of
-// one buffer), staged through this wave's LDS slot.  kOne (k_chunk): the
-// records are stored write-through (sc1), for walkers of the same launch.
-template <bool kMaskL, bool kFused, bool kOne>
+// one buffer), staged through this wave's LDS slot.
+template <bool kMaskL, bool kFused>
 __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, const Workspace &W, char *s_lds,
                                           const char *tab, uint32_t task, uint32_t lane, uint32_t wave,
                                           uint32_t laneoff)
@@ -605,9 +586,8 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     const uint64_t lo_ok = ub & ~15ull, hi_ok = (ub + D.len + 15) & ~15ull;  // 16-B blocks of the buffer
     const uint64_t seg0 = uint64_t(task - D.task_base) * 64u;               // first lane run of the task
     if (seg0 * sl >= D.len) return;                                          // alignment padding task
-    // this lane's tested range [s, e), buffer-relative
+    // this lane's run starts at s (buffer-relative); it tests [s, min(s + sl, len))
     const int64_t s = int64_t((seg0 + lane) * sl);
-    const int64_t e = s < int64_t(D.len) ? min(s + int64_t(sl), int64_t(D.len)) : s;
     // stage t of lane c covers [A(c) - 64 + kStage t, + kStage), A(c) = align16(ub + (seg0 + c) sl)
     // Staging starts kLead bytes before the run (>= W - 1 warm-up bytes); with
     // pair staging 128, so that its 128-B DMA chunks are whole HBM lines on a
@@ -636,33 +616,40 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     // Half 1's runs are 32 runs after half 0's (lane lengths are multiples of
     // 256 B, so the 16-B alignment commutes): its pieces are half 0's offsets
     // plus the uniform 32 sl, added to the SGPR base.
-    uint32_t off0[4];
+    // offi[j] = piece j's offset - 1024 j (dma_stage_imm); for j >= 1 the run
+    // is >= 8 runs (>= 4 KiB) past lane 0's, so the subtraction never wraps
+    uint32_t offi[4];
+    uint32_t om = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t r = 8u * j + lane / 8u;
         const uint32_t k = (lane % 8u) ^ ((r >> 1) & 7u);
-        off0[j] = uint32_t((((ub + (seg0 + r) * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
+        const uint32_t o = uint32_t((((ub + (seg0 + r) * sl) & ~15ull) - kLead + 16u * k) - base);  // wraps below base: clamped
+        om = max(om, o);
+        offi[j] = o - 1024u * j;
     }
-    const uint64_t om0 = scan_wave_max(max(max(off0[0], off0[1]), max(off0[2], off0[3])));
+    const uint64_t om0 = scan_wave_max(om);
     const uint64_t half_step = 32ull * sl;
-    auto issue = [&](auto PC, uint32_t u) {
+    // kFast: the caller knows the pieces stay inside the buffer (the steady loop)
+    auto issue = [&](auto PC, uint32_t u, auto FC) {
         constexpr uint32_t Q = decltype(PC)::value;  // u & 1: the half this DMA feeds
+        constexpr bool kFast = decltype(FC)::value;
         const uint64_t adv = uint64_t(kStage) * (u - Q) + (Q ? half_step : 0ull);
 #ifdef CDC_DIAG_NO_DMA
         return;  // build-time diagnostic only: no DMA (the slot keeps stale bytes), timing only
 #endif
-        if (om0 + adv <= uint64_t(lim)) {
+        if (kFast || om0 + adv <= uint64_t(lim)) {
 #ifdef CDC_DIAG_L2
             // build-time diagnostic only: every DMA reads a 512-KiB window of
             // the buffer (L2-resident), wrong bytes, the scan's compute alone
-            dma_stage(lo_ok + ((base + adv - lo_ok) & 0x7FFF0ull), ring, off0);
+            dma_stage_imm(lo_ok + ((base + adv - lo_ok) & 0x7FFF0ull), ring, offi);
 #else
-            dma_stage(base + adv, ring, off0);
+            dma_stage_imm(base + adv, ring, offi);
 #endif
         } else {
             uint32_t eff[4];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) eff[j] = min(off0[j] + uint32_t(adv), lim);
+            for (uint32_t j = 0; j < 4; ++j) eff[j] = min(offi[j] + 1024u * j + uint32_t(adv), lim);
             dma_stage(base, ring, eff);
         }
     };
@@ -686,13 +673,15 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
     using C0 = std::integral_constant<uint32_t, 0>;
     using C1 = std::integral_constant<uint32_t, 1>;
+    using Gen = std::integral_constant<bool, false>;
+    using Steady = std::integral_constant<bool, true>;
 
     uint4 A[4] = {}, Bv[4] = {};
 #ifdef CDC_DIAG_WAITS
     // build-time diagnostic only: shader cycles this wave spends in the
     // per-stage DMA waits, its whole task and where it ran, to g_ts[kTsRes + 8 task]
     uint64_t wsum = 0;
-    uint32_t nrc = 0;  // groups whose filter fired in some lane (wave-uniform branch count)
+    uint32_t nrc = 0;  // 32-byte groups whose filter fired in some lane (wave-uniform branch count)
     const uint64_t tk0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -700,16 +689,16 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     // the run, and stage 1 alone gives fp >= 64 >= W - 1 warm-up bytes.  Its
     // loads and DMA issues are kept.
     static_assert(kLead >= 2 * kStage, "stage 0 must be pure warm-up for both halves");
-    issue(C0{}, 0);
+    issue(C0{}, 0, Gen{});
     wait_vmcnt<0>();
     if (half == 0) load_row(A, Bv);  // stage 0 (unused) and stage 1 of half 0
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (1 < TT) issue(C1{}, 1);
+    if (1 < TT) issue(C1{}, 1, Gen{});
     if (1 < TT) {
         wait_vmcnt<0>();
         if (half == 1) load_row(Bv, A);  // stages 1 and 2 of half 1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (2 < TT) issue(C0{}, 2);
+        if (2 < TT) issue(C0{}, 2, Gen{});
     }
     uint64_t gv[2][16];
 #pragma unroll
@@ -717,16 +706,77 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     uint64_t fp = 0;
     uint64_t rec = 0;
     uint64_t recL = 0;  // k_scan_f: the run's MaskL record
-    const int32_t len = int32_t(e - s);
     const int32_t rr0 = int32_t(rel0 - s) - lag;
+    // The recheck queue.  A lane whose filter fired in a 32-byte group queues
+    // that group -- fp before it, its offset in the run and the lane: 12 bytes
+    // of LDS -- and the wave rechecks the queue, one item per lane, at the end
+    // of the task or when the queue is full.
+    // The group's bytes are read again from memory then (aligned 16-byte
+    // loads, clamped into the buffer; bytes outside the run only feed
+    // positions the valid mask drops), so nothing of the group has to stay in
+    // registers.  Rechecked in queue order, each run's hits reach its lane in
+    // position order (the record keeps its first kRunCap ascending).
+    uint64_t *const qf = reinterpret_cast<uint64_t *>(s_lds + kGearLdsBytes + kS2Waves * kStageBytes + wave * kQBytes);
+    uint32_t *const qm = reinterpret_cast<uint32_t *>(qf + kQCap);
+    static_assert(kQCap == 64, "one flush pass: item j in lane j");
+    uint32_t qn = 0;  // queued items (wave-uniform)
+    auto flush = [&]() {
+        {
+            const bool v = lane < qn;
+            const uint32_t meta = qm[v ? lane : 0u];
+            const uint32_t owner = meta >> 24;
+            const int32_t r0 = int32_t(meta & 0xFFFFFFu) - 256;
+            const int64_t so = int64_t((seg0 + owner) * sl);  // the owner's run [so, so + ln)
+            const int32_t ln = so < int64_t(D.len) ? int32_t(min(int64_t(sl), int64_t(D.len) - so)) : 0;
+            const uint64_t a = ub + uint64_t(so + r0);  // 16-B aligned
+            const uint64_t a0 = min(max(a, lo_ok), hi_ok - 16u), a1 = min(max(a + 16u, lo_ok), hi_ok - 16u);
+            const uint4 d0 = gload16(a0), d1 = gload16(a1);
+            uint64_t f = qf[v ? lane : 0u];
+            uint32_t miss = 0, missL = 0;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                f = (f << 1) + lds_gear(tab, gear_addr(laneoff, word_of(k < 16 ? d0 : d1, (k & 15) >> 2), k));
+                miss |= min(key_of(f, xlo, xhi), 1u) << k;
+                if constexpr (kFused)
+                    missL |= min(__builtin_amdgcn_alignbit(uint32_t(f >> 32), uint32_t(f), lws) & vlm, 1u) << k;
+            }
+            const int32_t lo = r0 < 0 ? -r0 : 0, hi = ln - r0;  // valid positions [0, ln) of the run
+            uint32_t vm = lo >= 32 ? 0u : (0xFFFFFFFFu << lo);
+            vm &= hi >= 32 ? 0xFFFFFFFFu : (hi <= 0 ? 0u : (1u << hi) - 1u);
+            const uint32_t hm = v ? ~miss & vm : 0u;
+            const uint32_t hmL = kFused && v ? ~missL & vm : 0u;
+            uint64_t todo = __ballot(hm != 0 || hmL != 0);  // false positives drop out here
+            while (todo) {
+                const int i = int(__builtin_ctzll(todo));
+                todo &= todo - 1;
+                const uint32_t o = uint32_t(__builtin_amdgcn_readlane(int(owner), i));
+                const int32_t ri = __builtin_amdgcn_readlane(r0, i);
+                uint32_t m = uint32_t(__builtin_amdgcn_readlane(int(hm), i));
+                uint32_t mL = kFused ? uint32_t(__builtin_amdgcn_readlane(int(hmL), i)) : 0u;
+                if (lane == o) {
+                    for (; m; m &= m - 1) record_hit(rec, ri + int32_t(__builtin_ctz(m)));
+                    if constexpr (kFused)
+                        for (; mL; mL &= mL - 1) record_hit(recL, ri + int32_t(__builtin_ctz(mL)));
+                }
+            }
+        }
+        qn = 0;
+    };
     // One stage t of parity Q: rolls cur (stage t's data); at its last group
     // the half loading stage t + 1 fills nxt (stage t + 1) and cur (t + 2),
-    // and once those reads retired the slot takes DMA t + 2.
-    auto stage = [&](auto PC, uint32_t t, uint4 (&cur_d)[4], uint4 (&nxt_d)[4]) {
+    // and once those reads retired the slot takes DMA t + 2.  The filter is
+    // reduced over 32-byte groups (two 16-byte groups): one wave-uniform
+    // branch per 32 bytes into the queue.
+    uint64_t f0 = 0;   // fp before the current 32-byte group
+    uint32_t acc = 0xFFFFFFFFu;
+    // SC (Steady): stage t + 2 exists and its DMA stays inside the buffer, so
+    // the stage runs with no bounds tests (the loop over stage pairs below).
+    auto stage = [&](auto PC, auto SC, uint32_t t, uint4 (&cur_d)[4], uint4 (&nxt_d)[4]) {
         constexpr uint32_t Q = decltype(PC)::value;
+        constexpr bool kSteady = decltype(SC)::value;
 #pragma unroll
         for (uint32_t gi = 0; gi < kGroups; ++gi) {
-            if (gi + 1 == kGroups && t + 1 < TT) {
+            if (gi + 1 == kGroups && (kSteady || t + 1 < TT)) {
 #ifdef CDC_DIAG_WAITS
                 const uint64_t w0 = __builtin_amdgcn_s_memtime();
                 wait_vmcnt<0>();  // DMA t + 1 landed
@@ -740,8 +790,10 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
             const uint4 nx = gi + 1 < kGroups ? cur_d[gi + 1] : nxt_d[0];
             uint64_t (&cg)[16] = gv[gi & 1];
             uint64_t (&ng)[16] = gv[(gi + 1) & 1];
-            const uint64_t f0 = fp;
-            uint32_t acc = 0xFFFFFFFFu, accL = 0xFFFFFFFFu;
+            if ((gi & 1) == 0) {
+                f0 = fp;
+                acc = 0xFFFFFFFFu;
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 // byte by byte: the next group's address and gather between the
@@ -760,51 +812,62 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
                     ng[k + 1] = lds_gear(tab, a1);
                     acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
                     if constexpr (kFused)
-                        accL = umin3(accL, l0, __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm);
+                        acc = umin3(acc, l0, __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm);
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (q == 1 && gi + 1 == kGroups && t + 2 < TT) {
+                if (q == 1 && gi + 1 == kGroups && (kSteady || t + 2 < TT)) {
                     asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // the row reads precede these 8 gathers
-                    issue(PC, t + 2);
+                    issue(PC, t + 2, SC);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+            if (gi & 1) {
 #ifndef CDC_DIAG_NO_RECHECK
+                const uint64_t fm = __ballot(acc == 0);
 #ifdef CDC_DIAG_WAITS
-            nrc += __builtin_amdgcn_readfirstlane(uint32_t(__ballot(acc == 0) != 0));
+                nrc += fm ? 1u : 0u;
 #endif
-            if (acc == 0) [[unlikely]]
-                recheck_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, xlo, xhi, rec);
+                if (fm) [[unlikely]] {  // queue the lanes' 32-byte groups
+                    const uint32_t nq = uint32_t(__popcll(fm));
+                    if (qn + nq > kQCap) flush();
+                    if (acc == 0) {
+                        const uint32_t idx =
+                            qn + __builtin_amdgcn_mbcnt_hi(uint32_t(fm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(fm), 0u));
+                        const int32_t r0 = rr0 + int32_t(kStage * t + 16u * (gi - 1));
+                        qf[idx] = f0;
+                        qm[idx] = uint32_t(r0 + 256) | (lane << 24);
+                    }
+                    qn += nq;
+                }
 #else
-            rec += acc == 0 ? 1u : 0u;  // build-time diagnostic only: no recheck
-            (void)f0;
-#if CDC_DIAG_NO_RECHECK == 2
-            if (acc == 0) [[unlikely]] asm volatile("s_nop 0" ::: "memory");  // the branch alone
-#endif
-#endif
-            if constexpr (kFused) {
-#ifndef CDC_DIAG_NO_LRECORD
-                if (accL == 0) [[unlikely]]
-                    record_l_group(f0, cg, rr0 + int32_t(kStage * t + 16u * gi), len, lws, vlm, recL);
-#else
-                recL += accL == 0 ? 1u : 0u;  // build-time diagnostic only: no MaskL records
+                rec += acc == 0 ? 1u : 0u;  // build-time diagnostic only: no recheck
 #endif
             }
         }
     };
-    if (1 < TT) stage(C1{}, 1, Bv, A);
-    for (uint32_t t = 2; t < TT; t += 2) {
-        stage(C0{}, t, A, Bv);
-        if (t + 1 < TT) stage(C1{}, t + 1, Bv, A);
+    if (1 < TT) stage(C1{}, Gen{}, 1, Bv, A);
+    // Steady pairs (t, t + 1): t + 3 < TT, and DMA t + 3 -- the farthest
+    // of the pair's, adv = 64 (t + 2) + 32 sl -- inside the buffer.  The
+    // stages after them (at most the last three, or all of a clamped wave's)
+    // test their bounds.
+    const int64_t room = int64_t(lim) - int64_t(om0) - int64_t(half_step);
+    const int64_t tf = room >= 128 ? room / 64 - 1 : 0;
+    const uint32_t t_steady = uint32_t(max<int64_t>(2, min<int64_t>(int64_t(TT) - 3, tf)));
+    uint32_t t = 2;
+    for (; t < t_steady; t += 2) {
+        stage(C0{}, Steady{}, t, A, Bv);
+        stage(C1{}, Steady{}, t + 1, Bv, A);
     }
-    if (s < int64_t(D.len)) put_rec((kMaskL ? W.runsL : W.runs) + 64ull * D.task_base + seg0 + lane, rec, kOne);
+    for (; t < TT; t += 2) {
+        stage(C0{}, Gen{}, t, A, Bv);
+        if (t + 1 < TT) stage(C1{}, Gen{}, t + 1, Bv, A);
+    }
+    if (qn) flush();
+    if (s < int64_t(D.len)) (kMaskL ? W.runsL : W.runs)[64ull * D.task_base + seg0 + lane] = rec;
     if constexpr (kFused) {
-        if (s < int64_t(D.len)) put_rec(W.runsL + 64ull * D.task_base + seg0 + lane, recL, kOne);
-        if (lane == 0) {
-            if constexpr (kOne) __hip_atomic_store(W.validL + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else W.validL[task] = 1u;
-        }
+        if (s < int64_t(D.len)) W.runsL[64ull * D.task_base + seg0 + lane] = recL;
+        if (lane == 0) W.validL[task] = 1u;
     }
     if (!kMaskL && lane == 0) dbg_ts(B, kTsScan + 4 * blockIdx.x + 2 + (wave & 1));  // end of waves 0 / 1
 #ifdef CDC_DIAG_WAITS
@@ -972,55 +1035,11 @@ struct WalkCtx {
     const uint64_t *gear;   // the 256-entry table in device memory
     const g_u64 *runsL;     // this buffer's MaskL index records (null: no MaskL index)
     const g_u32 *validL;    // per scan task of the buffer: runsL holds its 64 records
-    // k_chunk (records written by scan waves of the same launch): the buffer's
-    // per-task "records stored" flags, or null when the records were final
-    // before the launch; [dlo, dhi) tasks already seen done (wave-uniform).
-    const g_u32 *tdone;
-    mutable uint32_t dlo, dhi;
     uint32_t *flags;  // the launch's flags (the abort word: bounded waits)
 };
 
-// Wait until the scan tasks holding runs [r_lo, r_hi] of the buffer have
-// stored their records (k_chunk), 64 task flags per round trip.  Every task
-// waited on was claimed by a running wave whose scan never waits, so the wait
-// ends.  The records are then read write-through (ld_run).
-__device__ __forceinline__ void wait_runs(const WalkCtx &C, uint32_t t0, uint32_t t1)
-{
-    for (uint32_t b0 = t0; b0 <= t1; b0 += 64) {
-        const uint32_t t = b0 + C.lane;
-        SpinGuard sp;
-        for (;;) {
-            const uint32_t v = t <= t1 ? __hip_atomic_load(C.tdone + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
-            const uint64_t m = __ballot(v == 0u);
-            if (!m || !sp.ok(C.flags, kWaitTask, b0 + uint32_t(__ffsll((unsigned long long)m) - 1), t1)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    if (t0 <= C.dhi && t1 + 1 >= C.dlo) {  // extend the known range
-        C.dlo = min(C.dlo, t0);
-        C.dhi = max(C.dhi, t1 + 1);
-    } else {
-        C.dlo = t0;
-        C.dhi = t1 + 1;
-    }
-}
-
-template <bool kGate>
-__device__ __forceinline__ void ensure_runs(const WalkCtx &C, uint64_t r_lo, uint64_t r_hi)
-{
-    if constexpr (!kGate) return;
-    const uint32_t t0 = uint32_t(r_lo >> 6), t1 = uint32_t(r_hi >> 6);  // 64 runs per scan task
-    if (t0 >= C.dlo && t1 < C.dhi) return;
-    wait_runs(C, t0, t1);
-}
-
-// Run record q of the buffer (after ensure_runs when gated).
-template <bool kGate>
-__device__ __forceinline__ uint64_t ld_run(const g_u64 *runs, uint64_t q)
-{
-    if constexpr (kGate) return __hip_atomic_load(runs + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return runs[q];
-}
+// Run record q of the buffer.
+__device__ __forceinline__ uint64_t ld_run(const g_u64 *runs, uint64_t q) { return runs[q]; }
 
 // (A 32-copy table for long raw scans, filled on first use: C3 +2-4 %, C1 -4 %
 // from the 80-KiB workgroups; not kept.)
@@ -1156,15 +1175,13 @@ __device__ uint64_t recs_first(const WalkCtx &C, const DevParams &P, uint64_t r0
 }
 
 // First full-window MaskS candidate in [a, b) from the run index.
-template <bool kGate>
 __device__ __forceinline__ uint64_t index_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
     const uint64_t rl = run_of(C, b - 1);
     for (uint64_t r0 = run_of(C, a); r0 <= rl; r0 += 64) {
         const bool in = r0 + C.lane <= rl;
-        ensure_runs<kGate>(C, r0, min(rl, r0 + 63));
-        const uint64_t rec = in ? ld_run<kGate>(C.runs, r0 + C.lane) : 0ull;
+        const uint64_t rec = in ? ld_run(C.runs, r0 + C.lane) : 0ull;
         bool done;
         const uint64_t h = recs_first(C, P, r0, in, rec, a, b, fz, done);
         if (done) return h;
@@ -1176,7 +1193,6 @@ __device__ __forceinline__ uint64_t index_first_hit(const WalkCtx &C, const DevP
 // every window is full): from the MaskL index for the scan tasks k_scan_l
 // built (64 records per round trip, dense runs rescanned), by a raw scan for
 // the others.
-template <bool kGate>
 __device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevParams &P, uint64_t a, uint64_t b,
                                                  uint64_t fz)
 {
@@ -1184,13 +1200,9 @@ __device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevP
     const uint64_t ra = run_of(C, a), rl = run_of(C, b - 1);
     for (uint64_t r0 = ra & ~63ull; r0 <= rl; r0 += 64) {
         const uint64_t lo = max(a, r0 * C.sl), hi = min(b, (r0 + 64) * C.sl);
-        ensure_runs<kGate>(C, r0, r0);  // validL and runsL of task r0 / 64
-        uint32_t vl;
-        if constexpr (kGate) vl = __hip_atomic_load(C.validL + (r0 >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else vl = C.validL[r0 >> 6];
-        if (vl) {
+        if (C.validL[r0 >> 6]) {
             const bool in = r0 + C.lane >= ra && r0 + C.lane <= rl;
-            const uint64_t rec = in ? ld_run<kGate>(C.runsL, r0 + C.lane) : 0ull;
+            const uint64_t rec = in ? ld_run(C.runsL, r0 + C.lane) : 0ull;
             bool done;
             const uint64_t h = recs_first(C, P, r0, in, rec, lo, hi, fz, done, true);
             if (done) return h;
@@ -1208,7 +1220,6 @@ __device__ __forceinline__ uint64_t maskl_first_hit(const WalkCtx &C, const DevP
 // Common case in ONE global round trip: every lane issues, together, its
 // truncated-window byte, the candidate count of one index block and two
 // entries of the first two blocks.
-template <bool kGate>
 __device__ __forceinline__ uint64_t next_node(const WalkCtx &C, const DevParams &P, uint64_t p)
 {
     const uint64_t E = C.len, r = E - p;
@@ -1246,8 +1257,7 @@ __device__ __forceinline__ uint64_t next_node(const WalkCtx &C, const DevParams 
     uint32_t byte = 0;
     uint64_t rec = 0;
     if (tvalid) byte = as_space<const g_u8>(C.ub)[tpos];
-    if (has_s) ensure_runs<kGate>(C, r0, min(rl, r0 + 63));
-    if (rin) rec = ld_run<kGate>(C.runs, r0 + j);
+    if (rin) rec = ld_run(C.runs, r0 + j);
     // ---- truncated window [fz, fz + W - 1)
     uint64_t h = trunc_first_hit(C, P, fz, norm_end, lim, byte);
     if (h != kNoHit) return h + P.cut_adj;
@@ -1257,14 +1267,14 @@ __device__ __forceinline__ uint64_t next_node(const WalkCtx &C, const DevParams 
         h = recs_first(C, P, r0, rin, rec, full0, s_end, fz, done);
         if (done) return h + P.cut_adj;
         if (r0 + 64 <= rl) {
-            h = index_first_hit<kGate>(C, P, (r0 + 64) * C.sl, s_end, fz);
+            h = index_first_hit(C, P, (r0 + 64) * C.sl, s_end, fz);
             if (h != kNoHit) return h + P.cut_adj;
         }
     }
     // ---- MaskL region [p + Normal, p + n): the MaskL index, or a raw scan
     const uint64_t l_lo = max(norm_end, full0);
     if (l_lo < lim) {
-        h = maskl_first_hit<kGate>(C, P, l_lo, lim, fz);
+        h = maskl_first_hit(C, P, l_lo, lim, fz);
         if (h != kNoHit) return h + P.cut_adj;
     }
     return clipped ? kUndet : p + n;
@@ -1476,7 +1486,6 @@ __device__ __forceinline__ uint32_t graph_lookup(const Graph &G, uint32_t lane, 
 }
 
 // Build the graph of segment [S0, S1): list, preload, successors.
-template <bool kGate>
 __device__ __forceinline__ void graph_build(const WalkCtx &C, const DevParams &P, GraphLds &L, Graph &G, uint64_t S0, uint64_t S1,
                             const Batch &B, uint32_t tslot)
 {
@@ -1488,11 +1497,10 @@ __device__ __forceinline__ void graph_build(const WalkCtx &C, const DevParams &P
     const uint64_t rneed = run_of(C, min(C.len, S1 + P.normal_size) - 1);
     const uint32_t nr = uint32_t(min<uint64_t>(rneed - ra + 1, kGRecs));
     uint64_t recs[kGRecs / 64];
-    ensure_runs<kGate>(C, ra, ra + nr - 1);
 #pragma unroll
     for (uint32_t k = 0; k < kGRecs / 64; ++k) {
         const uint32_t i = 64u * k + lane;
-        recs[k] = 64u * k < nr && i < nr ? ld_run<kGate>(C.runs, ra + i) : 0ull;
+        recs[k] = 64u * k < nr && i < nr ? ld_run(C.runs, ra + i) : 0ull;
     }
     uint32_t n = 1;  // node 0: the segment start (the speculative chain's first node)
     if (lane == 0) L.node[0] = S0;
@@ -1585,9 +1593,6 @@ __device__ __forceinline__ WalkCtx make_ctx(const Batch &B, const BufDesc &D, co
     C.gear = W.gear;
     C.runsL = B.maskl_index ? as_space<const g_u64>(reinterpret_cast<uintptr_t>(W.runsL + 64ull * D.task_base)) : nullptr;
     C.validL = B.maskl_index ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.validL + D.task_base)) : nullptr;
-    C.tdone = B.one_launch ? as_space<const g_u32>(reinterpret_cast<uintptr_t>(W.tdone + D.task_base)) : nullptr;
-    C.dlo = 0;
-    C.dhi = 0;
     C.flags = W.flags;
     return C;
 }
@@ -1632,6 +1637,7 @@ constexpr uint32_t kMaxList = 64;                // nodes per register list
 constexpr uint64_t kX55 = (1ull << 55) - 1;      // xg: X in bits 0-54 (all ones: kUndet), node count 55-61,
 constexpr uint64_t kXNodes = 1ull << 62;         //     62: the node list is readable, 63: X is published
 constexpr uint64_t kKindLocal = 1ull << 62, kKindIncl = 2ull << 62;
+constexpr uint64_t kKindAbort = 3ull << 62;      // a wait of this segment (or below it) gave up: E = end, O = 0
 constexpr uint32_t kConvEnd = 0x3FFFFFu;         // LOCAL: the chain ends in this piece (or before it)
 constexpr uint32_t kSegEnd = 0xFFFFFFu;          // INCLUSIVE: no further segment on the chain
 
@@ -1718,7 +1724,7 @@ __device__ __forceinline__ uint32_t row_incl_sum32(uint32_t x)
 }
 
 __device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t lane, uint32_t &E, uint64_t &O,
-                                      uint32_t *flags)
+                                      uint32_t *flags, bool &ab)
 {
     uint32_t Fe = q + lane;  // F, lane t < kJ: entering at hi + 1 + t leaves E = Fe with Fo cuts added
     uint64_t Fo = 0;
@@ -1743,14 +1749,15 @@ __device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t l
                     if (!sp.ok(flags, kWaitLook, q, uint64_t(lo0))) {
                         E = kSegEnd;  // gave up: the launch reports CDC_E_DEVICE
                         O = 0;
+                        ab = true;
                         return;
                     }
                     __builtin_amdgcn_s_sleep(kSpinSleep);
                     if (valid && !s) s = ld_rlx(sg + p);
                 }
             }
-            const uint64_t im = __ballot(valid && (s >> 62) == 2);
-            const int istar = im ? 63 - int(__builtin_clzll(im)) : -1;  // nearest INCLUSIVE (segment 0 always is)
+            const uint64_t im = __ballot(valid && (s >> 62) >= 2);
+            const int istar = im ? 63 - int(__builtin_clzll(im)) : -1;  // nearest INCLUSIVE / ABORTED (segment 0 always is)
             const bool rel = valid && int(lane) > istar;
             const uint32_t code = uint32_t((s >> 40) & 0x3FFFFFu);
             const uint64_t cnt = rel ? (s & ((1ull << 40) - 1)) : 0ull;
@@ -1795,6 +1802,12 @@ __device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t l
             }
             if (istar >= 0) {
                 const uint64_t si = readlane64(s, istar);
+                if ((si >> 62) == 3) {  // aborted below: so is this segment
+                    E = kSegEnd;
+                    O = 0;
+                    ab = true;
+                    return;
+                }
                 const uint32_t ep = uint32_t((si >> 38) & 0xFFFFFFu);
                 const uint64_t op = si & ((1ull << 38) - 1);
                 if (ep == kSegEnd) {
@@ -1820,41 +1833,62 @@ __device__ __noinline__ void lookback(const uint64_t *sg, uint32_t q, uint32_t l
 slow_path:  // q - 1's own INCLUSIVE status
     uint64_t sq;
     SpinGuard sp;
-    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) != 2) {
+    while (((sq = readlane64(ld_rlx(sg + q - 1), 0)) >> 62) < 2) {
         if (!sp.ok(flags, kWaitLookSlow, q, 0)) {
             E = kSegEnd;
             O = 0;
+            ab = true;
             return;
         }
         __builtin_amdgcn_s_sleep(kSpinSleep);
+    }
+    if ((sq >> 62) == 3) {
+        E = kSegEnd;
+        O = 0;
+        ab = true;
+        return;
     }
     E = uint32_t((sq >> 38) & 0xFFFFFFu);
     O = sq & ((1ull << 38) - 1);
 }
 
+// A result row's status, settled once: the scan kernel marks every row
+// pending, the buffer's last segment turns pending into its status, and a
+// wave whose wait gave up stores CDC_E_DEVICE into every row of the launch
+// group (after or before the last segment: the row ends CDC_E_DEVICE).
+__device__ __forceinline__ void settle_row(cdc_result *res, int64_t st)
+{
+    int64_t pend = kRowPending;
+    __hip_atomic_compare_exchange_strong(&res->status, &pend, st, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __noinline__ void abort_rows(const Batch &B, uint32_t lane)
+{
+    for (uint32_t i = lane; i < B.nbufs; i += 64)
+        __hip_atomic_store(&B.b[i].res->status, int64_t(CDC_E_DEVICE), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The sequential walk of a whole buffer (debug mode, lists that overflow):
 // one wave walks next() from offset 0 and writes the cut list and the result row.
-template <bool kGate>
 __device__ __forceinline__ void resolve_sequential(const WalkCtx &C, const DevParams &P, const BufDesc &D)
 {
     uint64_t p = 0, idx = 0;
     while (p < C.len) {
-        const uint64_t nx = next_node<kGate>(C, P, p);
+        const uint64_t nx = next_node(C, P, p);
         if (nx == kUndet) break;
         if (C.lane == 0 && idx < D.cap) put_cut(D.out + idx, p, nx - p);
         ++idx;
         p = nx;
     }
     if (C.lane == 0) {
-        uint64_t *r = reinterpret_cast<uint64_t *>(D.res);
         st_rlx(&D.res->ncuts, idx <= D.cap ? idx : D.cap);
         st_rlx(&D.res->consumed, p);
-        st_rlx(r + 2, uint64_t(int64_t(idx <= D.cap ? CDC_OK : CDC_E_NOSPACE)));
         st_rlx(&D.res->needed, idx);
+        settle_row(D.res, idx <= D.cap ? CDC_OK : CDC_E_NOSPACE);
     }
 }
 
-template <bool kGate>
 __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams &P, const Workspace &W, uint32_t g,
                                                 const char *tab, GraphLds L)
 {
@@ -1866,9 +1900,12 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     const bool l0 = lane == 0;
     if (l0) dbg_ts(B, kTsRes + 8 * g);
     Graph G;
-    graph_build<kGate>(C, P, L, G, S0, S1, B, kTsRes + 8 * g);
+    graph_build(C, P, L, G, S0, S1, B, kTsRes + 8 * g);
     if (l0) dbg_ts(B, kTsRes + 8 * g + 1);
     bool ovf = false;
+    // debug mode 2: buffer 0's first segment never publishes its exit, so its
+    // successor's wait for it gives up (the device-abort path)
+    const bool withhold = (B.debug & kDbgForceAbort) && g == 0 && D.nseg > 1;
     // ---- A (phase 0) and B (phase 1).  While the walk stays on listed nodes
     // of a graph that fits one register (n <= 64: every 1-MiB segment of
     // random data), it is a scalar loop over node indices collecting a bit
@@ -1876,6 +1913,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     // kGHard node, an unlisted successor, another segment) goes through the
     // general loop: the graph where it answers, next_node() elsewhere.
     const bool g64 = G.n <= 64;
+    bool aborted = false;  // a bounded wait of this wave gave up (or saw the launch's abort word)
     uint64_t sv = kUndet, jv = kUndet, cv = kUndet;  // lane i: node i of the speculative chain / junction / merged-into list
     uint32_t ns = 0, c2 = 0, cns = 0, k = 0, cur = q, conv = kConvEnd, exact = 0;
     uint64_t X = kUndet, cX = kUndet, ex = kUndet;  // ex: the node after the piece
@@ -1919,7 +1957,12 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
             }
             const uint64_t xp = wait_granule(W.xg + g - 1, W.flags, g);  // its load drained this wave's node-list stores
             drain_stores();
-            if (l0) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
+            if (l0 && !withhold) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
+            if (!xp) {  // gave up: no entry, no piece
+                aborted = true;
+                ex = kUndet;
+                break;
+            }
             x = x_dec(xp);
             cur = q;
             cv = sv;
@@ -1975,18 +2018,16 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                     if (phase == 1) {
                         const uint64_t r = x / seg;
                         if (r != cur) {  // entered a later segment: its published speculative chain
-                            // (k_chunk waits only for a segment some running wave
-                            // has taken: phase A never waits for a later one, so
-                            // the wait ends; an untaken segment is walked through)
+                            // (phase A never waits, so the wait ends)
                             uint64_t xr;
                             SpinGuard sp;
                             for (;;) {
                                 xr = readlane64(ld_rlx(W.xg + base + r), 0);
                                 if (xr & kXNodes) break;
-                                if (kGate &&
-                                    __hip_atomic_load(W.tick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= base + r)
+                                if (!sp.ok(W.flags, kWaitJunction, g, base + r)) {
+                                    aborted = true;
                                     break;
-                                if (!sp.ok(W.flags, kWaitJunction, g, base + r)) break;
+                                }
                                 __builtin_amdgcn_s_sleep(kSpinSleep);
                             }
                             cur = uint32_t(r);
@@ -2029,7 +2070,7 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
                 if (s != kGHard) {
                     nx = s;
                 } else {
-                    nx = next_node<kGate>(C, P, x);
+                    nx = next_node(C, P, x);
                     ni = nx < segE ? graph_lookup(G, lane, nx) : kGNone;
                     ++exact;
                 }
@@ -2043,13 +2084,13 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
             // X at once; the node list (read only by junctions that cross into this
             // segment) is flagged readable once a later load has drained its stores
             if (lane < ns) st_rlx(W.w1_nodes + size_t(g) * kMaxList + lane, sv);
-            if (l0) {
+            if (l0 && !withhold) {
                 st_rlx(W.xg + g, x_enc(X, ns));
                 dbg_ts(B, kTsRes + 8 * g + 2);
             }
             if (q == 0) {
                 drain_stores();
-                if (l0) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
+                if (l0 && !withhold) st_rlx(W.xg + g, x_enc(X, ns) | kXNodes);
             }
         }
     }
@@ -2060,12 +2101,12 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     if (ovf && l0) __hip_atomic_store(W.flags + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t E = 0;
     uint64_t O = 0;
-    if (q > 0) {
+    if (q > 0 && !aborted) {
         if (l0) st_rlx(W.sg + g, kKindLocal | (uint64_t(conv == kConvEnd ? kConvEnd : conv - q) << 40) | cuts);
-        lookback(sgb, q, lane, E, O, W.flags);
+        lookback(sgb, q, lane, E, O, W.flags, aborted);
     }
     if (l0) dbg_ts(B, kTsRes + 8 * g + 3);
-    const bool on = E == q;
+    const bool on = E == q && !aborted;
     const bool fb = B.force_fallback != 0;
     if (on && !fb && nodes > 0) {
         auto node_at = [&](uint32_t u) -> uint64_t {
@@ -2089,6 +2130,11 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
     }
     const uint32_t Eq = on ? (conv == kConvEnd ? kSegEnd : conv + 1) : E;
     const uint64_t Oq = O + (on ? cuts : 0ull);
+    if (aborted) {  // an ABORTED status (look-back passes it up) and CDC_E_DEVICE in every row
+        if (l0) st_rlx(W.sg + g, kKindAbort);
+        abort_rows(B, lane);
+        return;
+    }
     if (l0) {
         st_rlx(W.sg + g, kKindIncl | (uint64_t(Eq) << 38) | Oq);
         dbg_ts(B, kTsRes + 8 * g + 4);
@@ -2104,22 +2150,28 @@ __device__ __forceinline__ void resolve_segment(const Batch &B, const DevParams 
         for (uint32_t p0 = 0; p0 < q; p0 += 64) {
             const uint32_t p = p0 + lane;
             SpinGuard sp;
-            while (__ballot(p < q && (ld_rlx(sgb + min(p, q - 1)) >> 62) != 2)) {
-                if (!sp.ok(W.flags, kWaitLast, g, p0)) break;
+            while (__ballot(p < q && (ld_rlx(sgb + min(p, q - 1)) >> 62) < 2)) {
+                if (!sp.ok(W.flags, kWaitLast, g, p0)) {
+                    aborted = true;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(kSpinSleep);
+            }
+            if (aborted || __ballot(p < q && (ld_rlx(sgb + min(p, q - 1)) >> 62) == 3)) {
+                abort_rows(B, lane);
+                return;
             }
         }
         if (__hip_atomic_load(W.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || fb) {
-            resolve_sequential<kGate>(C, P, D);
+            resolve_sequential(C, P, D);
             return;
         }
     }
     if (l0) {
-        uint64_t *r = reinterpret_cast<uint64_t *>(D.res);
         const bool ab = __hip_atomic_load(W.flags + kAbortWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         st_rlx(&D.res->ncuts, Oq <= D.cap ? Oq : D.cap);
-        st_rlx(r + 2, uint64_t(int64_t(ab ? CDC_E_DEVICE : Oq <= D.cap ? CDC_OK : CDC_E_NOSPACE)));
         st_rlx(&D.res->needed, Oq);
+        settle_row(D.res, ab ? CDC_E_DEVICE : Oq <= D.cap ? CDC_OK : CDC_E_NOSPACE);
     }
 }
 
@@ -2130,8 +2182,9 @@ __device__ __forceinline__ void write_empty_rows(const Batch &B, uint32_t lane)
         if (B.b[i].nseg == 0) {
             B.b[i].res->ncuts = 0;
             B.b[i].res->consumed = 0;
-            B.b[i].res->status = CDC_OK;
             B.b[i].res->needed = 0;
+            if (B.total_tasks) settle_row(B.b[i].res, CDC_OK);  // marked pending by the scan kernel
+            else B.b[i].res->status = CDC_OK;                   // no scan kernel ran
         }
     }
 }
@@ -2150,7 +2203,7 @@ __global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B,
     if (blockIdx.x == 0 && wave == 0) write_empty_rows(B, lane);
     const uint32_t g = uint32_t(__builtin_amdgcn_readfirstlane(s_ticket)) * kWalkWavesPerWG + wave;
     if (g < B.total_segs)
-        resolve_segment<false>(B, P, W, g, reinterpret_cast<const char *>(s_tab), graph_lds(s_grec[wave], s_gx[wave]));
+        resolve_segment(B, P, W, g, reinterpret_cast<const char *>(s_tab), graph_lds(s_grec[wave], s_gx[wave]));
 }
 
 // ---------------------------------------------------------------------------
@@ -2288,166 +2341,6 @@ int launch_stream_read(const void *d_buf, uint64_t len, int reps, double *best_u
 }
 
 // ---------------------------------------------------------------------------
-// k_chunk: the scan and the chain resolution of a launch group in ONE launch
-// (k_chunk_f: with the MaskL index fused into the scan, as k_scan_f).  Workgroups as k_scan's (12 waves,
-// one per CU); every wave first scans, then resolves:
-//
-//   * Scan tasks are claimed, not assigned: the waves of a SIMD finish in age
-//     order (the oldest first: DESIGN.md 5.1, round 4), so wave w of a
-//     workgroup claims from tier w / 4's counter, and tier k holds the k-th
-//     third of the launch group's tasks.  The buffer's first third is then
-//     final when the oldest waves end, the last third when the youngest do.
-//     A wave whose tier is used up claims from the others (a workgroup that
-//     starts late, its CU held by another stream's kernel, finds its tasks
-//     taken).  After its task a wave stores its records write-through, drains
-//     them and raises the task's flag (tdone).
-//   * Resolution segments are claimed in order (W.tick[0]) only once every
-//     scan task is claimed, and k_resolve's phases run on them (issue
-//     priority below the scan, which sets the critical path).  A walker
-//     waits for the flags of the tasks whose records it reads (ensure_runs);
-//     a junction waits for a later segment's speculative chain only if a
-//     running wave has taken that segment.  Every wait is therefore on a
-//     running wave that will not wait on it: no deadlock whatever the
-//     residency (the other stream's kernel may hold any CUs).
-//
-// The segments of the first two thirds are resolved while the younger waves
-// still scan; only the last third's resolution follows the last scan task.
-// The host zeroes xg .. tdone (counters, flags, granules) before the launch.
-// LDS: the scan's 64-KiB shifted Gear table and 12 x 4-KiB slots (a wave's
-// slot then holds its graph's run records), the walkers' 16-KiB table, and
-// 12 x 1,088 B of graph bits and nodes: 141 KiB.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kTiers = kS2Waves % 3 == 0 ? 3 : 1;
-static_assert(kGRecs * 8 <= kStageBytes, "a wave's graph records fit its scan slot");
-
-// Claim word p for this wave: every lane takes part (lane 0 ORs 1, the
-// others 0, so no lane-0 branch precedes the readfirstlane, see wave_ticket);
-// true if this wave set it.
-__device__ __forceinline__ bool wave_claim(uint32_t *p)
-{
-    const uint32_t old = __hip_atomic_fetch_or(p, (threadIdx.x & 63u) == 0u ? 1u : 0u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane(old) == 0u;
-}
-
-constexpr uint32_t kStartShards = 8;  // k_chunk: "tasks taken" counter, sharded by task % 8 (tick[8 .. 16))
-constexpr uint32_t kTickClaims = 16;  // k_chunk: per-task claim words from tick[16]
-
-__device__ __forceinline__ uint32_t tasks_taken(const uint32_t *shards)
-{
-    const uint32_t l = threadIdx.x & 63u;
-    const uint32_t v = l < kStartShards ? __hip_atomic_load(shards + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    uint32_t sum = v;
-#pragma unroll
-    for (int o = 4; o; o >>= 1) sum += uint32_t(__shfl_xor(int(sum), o));
-    return __builtin_amdgcn_readfirstlane(sum);
-}
-
-template <bool kFused>
-__device__ __forceinline__ void chunk_body(const Batch &B, const DevParams &P, const Workspace &W)
-{
-    // one array, in a fixed order: the scan's table and slots first, at the
-    // LDS offsets k_scan uses (its slots' LDS-DMA bases below 112 KiB)
-    constexpr uint32_t kScanLds = kGearLdsBytes + kS2Waves * kStageBytes;
-    __shared__ __attribute__((aligned(16))) char s_all[kScanLds + 256 * kWCopies * 8 + kS2Waves * kGExtra * 8];
-    char *const s_lds = s_all;
-    uint64_t *const s_wtab = reinterpret_cast<uint64_t *>(s_all + kScanLds);
-    uint64_t *const s_gx0 = s_wtab + 256 * kWCopies;  // wave w's graph bits and nodes at s_gx0 + w kGExtra
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t laneoff = (lane & 31u) << 3;
-    const uint32_t T = B.total_tasks;
-    uint32_t *const shards = W.tick + 8;
-    uint32_t *const claim = W.tick + kTickClaims;
-    // Static ownership: workgroup w's wave j owns task tier(j) tpt + 4 w +
-    // j % 4 (tier k = wave age k on its SIMD; tier k holds the k-th third of
-    // the tasks).  The claim (a word per task, no contention) flies while the
-    // tables fill.
-    constexpr uint32_t kPerTier = kS2Waves / kTiers;
-    const uint32_t tpt = gridDim.x * kPerTier;
-#ifdef CDC_CHUNK_MAP_LINEAR
-    const uint32_t mine = blockIdx.x * kS2Waves + wave;  // build-time A/B: k_scan's mapping
-    (void)tpt;
-#else
-    const uint32_t mine = (wave / kPerTier) * tpt + blockIdx.x * kPerTier + wave % kPerTier;
-#endif
-    bool own = false;
-    if (mine < T) own = wave_claim(claim + mine);
-    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, P.fs_sh);
-    fill_gear_lds<kS2Waves * 64, kWCopies>(s_wtab, W.gear);
-    if (blockIdx.x == 0 && wave == 0) write_empty_rows(B, lane);
-    __syncthreads();
-#ifndef CDC_CHUNK_NO_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
-    auto scan_one = [&](uint32_t task) {
-        if (lane == 0) __hip_atomic_fetch_add(shards + task % kStartShards, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t ts0 = (B.debug & kDbgTs) ? __builtin_amdgcn_s_memrealtime() : 0;
-        scan_task<false, kFused, true>(B, P, W, s_lds, s_lds, task, lane, wave, laneoff);
-        drain_stores();
-        if (lane == 0) __hip_atomic_store(W.tdone + task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((B.debug & kDbgTs) && lane == 0 && task < kTsTasks) {
-            uint64_t *o = g_ts + kTsTask + 4 * task;
-            o[0] = ts0;
-            o[1] = __builtin_amdgcn_s_memrealtime();
-            o[2] = wave;
-            o[3] = uint64_t(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11))) << 32 |
-                   uint32_t(__builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)));
-        }
-    };
-    if (own) scan_one(mine);
-    // Every task must be taken by a running wave before any walker waits: a
-    // task whose workgroup is not yet dispatched (its CU held by another
-    // stream's kernel) is taken by a wave that is done (only under such
-    // contention; the counter's adds fly while the tasks are scanned).
-    for (SpinGuard sp;;) {
-        if (tasks_taken(shards) >= T) break;
-        bool took = false;
-        for (uint32_t t0 = 0; t0 < T; t0 += 64) {
-            const uint32_t t = t0 + lane;
-            const uint32_t c = t < T ? __hip_atomic_load(claim + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
-            uint64_t m = __ballot(c == 0u);
-            while (m) {
-                const uint32_t v = t0 + uint32_t(__ffsll((unsigned long long)m) - 1);
-                m &= m - 1;
-                if (wave_claim(claim + v)) {
-                    scan_one(v);
-                    took = true;
-                    break;
-                }
-            }
-            if (took) break;
-        }
-        if (took) continue;
-        if (!sp.ok(W.flags, kWaitTask, T, 0)) break;  // every task claimed, the count not yet seen
-        __builtin_amdgcn_s_sleep(kSpinSleep);
-    }
-    // the walkers' latency-bound work issues ahead of the remaining scans
-#ifndef CDC_CHUNK_NO_PRIO
-    __builtin_amdgcn_s_setprio(2);
-#endif
-    if (B.debug & kDbgScanOnly) return;
-    const GraphLds L = graph_lds(s_lds + kGearLdsBytes + wave * kStageBytes, s_gx0 + wave * kGExtra);
-    for (;;) {
-        const uint32_t g = wave_ticket(W.tick);
-        if (g >= B.total_segs) break;
-        resolve_segment<true>(B, P, W, g, reinterpret_cast<const char *>(s_wtab), L);
-    }
-}
-
-__global__ __launch_bounds__(kS2Waves * 64) void k_chunk(const Batch B, const DevParams P, const Workspace W)
-{
-    chunk_body<false>(B, P, W);
-}
-
-// k_chunk with both indexes built in the scan (k_scan_f's body): a launch
-// group that needs the MaskL index, where the masks admit the fused window.
-__global__ __launch_bounds__(kS2Waves * 64) void k_chunk_f(const Batch B, const DevParams P, const Workspace W)
-{
-    chunk_body<true>(B, P, W);
-}
-
-// ---------------------------------------------------------------------------
 // Host side: planning and launching.
 // ---------------------------------------------------------------------------
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -2547,10 +2440,8 @@ int make_plan(const uint64_t *lens, int nbufs, const DevParams &P, Plan *plan)
     plan->off_xg = take(segs * 8);
     plan->off_sg = take(segs * 8);
     plan->off_flags = take((kMaxBufsPerLaunch + 4) * 4);  // per buffer + the abort word
-    // [0] segment ticket, [2] persistent scan task counter, [8 .. 16) k_chunk
-    // "tasks taken" shards, [16 ..] k_chunk per-task claims
-    plan->off_tick = take((16 + tasks) * 4);
-    plan->off_tdone = take(tasks * 4);
+    // [0] segment ticket, [2] persistent scan task counter
+    plan->off_tick = take(16 * 4);
     plan->off_runsL = take(tasks * 64 * 8);
     plan->off_validL = take(tasks * 4);
     plan->bytes = off;
@@ -2593,32 +2484,6 @@ int launch_batch(const Batch &B, const DevParams &P, const Workspace &W, void *s
     // With profiling on, the events ride on the kernels' own dispatch packets
     // (hipExtLaunchKernelGGL): no extra barrier packets, no bubbles.
     const uint32_t need_wgs = (B.total_tasks + kS2Waves - 1) / kS2Waves;
-    if (B.one_launch) {  // k_chunk: counters, flags and granules zeroed, then one kernel
-        const size_t zb = size_t(reinterpret_cast<char *>(W.tdone + B.total_tasks) - reinterpret_cast<char *>(W.xg));
-        if (hipMemsetAsync(W.xg, 0, zb, st) != hipSuccess) return CDC_E_DEVICE;
-        // one task per wave (a late workgroup's tasks are taken by waves that
-        // are done, so the grid needs no persistent form)
-        const uint32_t wgs = need_wgs > 0 ? need_wgs : 1u;
-        if (prof) {
-            if (B.maskl_index)
-                hipExtLaunchKernelGGL(k_chunk_f, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
-            else
-                hipExtLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, pr.e0, pr.e1, 0, B, P, W);
-            std::lock_guard<std::mutex> lk(g_prof_mu);
-            (void)hipEventRecord(pr.e2, st);
-            g_prof_live.push_back(pr);
-        } else {
-            if (B.maskl_index)
-                hipLaunchKernelGGL(k_chunk_f, dim3(wgs), dim3(kS2Waves * 64), 0, st, B, P, W);
-            else
-                hipLaunchKernelGGL(k_chunk, dim3(wgs), dim3(kS2Waves * 64), 0, st, B, P, W);
-        }
-        // the adaptive MaskL probe reads this launch's records; it only sets the hint for later groups
-        if (B.total_tasks > 0 && B.maskl_probe)
-            hipLaunchKernelGGL(k_maskl_probe, dim3((B.total_tasks + kProbeWaves - 1) / kProbeWaves),
-                               dim3(kProbeWaves * 64), 0, st, B, P, W);
-        return hipGetLastError() == hipSuccess ? CDC_OK : CDC_E_DEVICE;
-    }
     const dim3 sgrid(B.persist && B.scan_wgs < need_wgs ? B.scan_wgs : need_wgs), sblock(kS2Waves * 64);
     const bool fused = B.maskl_index && B.maskl_fused;  // k_scan_f: both indexes in one pass
     if (B.persist && B.total_tasks > 0 && hipMemsetAsync(W.tick + 2, 0, 4, st) != hipSuccess) return CDC_E_DEVICE;

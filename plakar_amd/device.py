@@ -95,13 +95,6 @@ def set_maskl_index_mode(mode):
     check(lib().cdc_set_maskl_index_mode(int(mode)))
 
 
-def set_resolve_mode(mode):
-    """0 = two launches (k_scan + k_resolve, the default), 1 = the scan and
-    the chain resolution in one launch (k_chunk; measured slower, DESIGN.md
-    5.3). Cut points do not depend on it."""
-    check(lib().cdc_set_resolve_mode(int(mode)))
-
-
 def maskl_state(device=0):
     """Adaptive MaskL state (diagnostics): (1 while the next launch groups
     build the MaskL index because a recent group asked for MaskL candidates,

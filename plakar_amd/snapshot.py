@@ -359,11 +359,6 @@ class BackupSession:
         errors = []
 
         def on_file(_ctx, fp):
-            # The callback creates a few objects per file; no cyclic
-            # collection (none of them forms a cycle) runs over the whole
-            # heap meanwhile.  Only this thread's callback is covered.
-            gc_was = gc.isenabled()
-            gc.disable()
             try:
                 f = fp.contents
                 i = int(f.index)
@@ -392,9 +387,6 @@ class BackupSession:
                                     ContentType=ctypes_of.pop(i, ""), Entropy=float(f.object_entropy))
             except Exception as e:  # noqa: BLE001 - re-raised after the call
                 errors.append(e)
-            finally:
-                if gc_was:
-                    gc.enable()
 
         def on_pack(_ctx, data, length):
             packs.append(ctypes.string_at(data, length) if keep_packfiles else None)
@@ -402,7 +394,17 @@ class BackupSession:
 
         fcb, pcb = _lib.BACKUP_FILE_FN(on_file), _lib.BACKUP_PACK_FN(on_pack)
         st = _lib.cdc_backup_stats()
-        rc = _lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st))
+        # The callbacks create a few objects per file, none of them in a
+        # cycle.  The cyclic collector is off for the whole call (gc.disable
+        # is process-wide): a collection triggered by those allocations would
+        # walk the whole heap between callbacks.
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            rc = _lib.lib().cdc_backup_files(self._h, arr, n, fcb, pcb, None, ctypes.byref(st))
+        finally:
+            if gc_was:
+                gc.enable()
         _lib.check(rc, "cdc_backup_files")
         if errors:
             raise errors[0]

@@ -216,6 +216,35 @@ def test_backup_large_file_failing_in_a_middle_piece(tmp_path, monkeypatch):
     assert {c.Checksum for o in objs[1:] for c in o.Chunks} <= stored
 
 
+def test_backup_device_failure_in_a_middle_piece(tmp_path, monkeypatch):
+    """A large file whose third piece's launch group aborts on the device (the
+    hook CDC_BACKUP_FAIL_DEVICE=file:piece runs that launch in debug mode 2:
+    a bounded wait gives up, every result row reports CDC_E_DEVICE).  The
+    backup returns CDC_E_DEVICE -- the reference aborts a backup on a chunker
+    error (snapshot/backup.go:98-101) -- instead of publishing a stale carry
+    to the next piece's reader; the same session then backs up the same files
+    intact."""
+    files = [random_bytes(70 << 20, 54).tobytes(), random_bytes(1 << 20, 55).tobytes(),
+             random_bytes(40 << 20, 56).tobytes()]
+    paths = []
+    for i, b in enumerate(files):
+        p = tmp_path / f"d{i}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    with snapshot.BackupSession(key=KEY, batch_bytes=8 << 20, packers=2) as s:
+        monkeypatch.setenv("CDC_BACKUP_FAIL_DEVICE", "0:2")
+        with pytest.raises(_lib.CdcError) as e:
+            s.run(paths)
+        assert e.value.status == _lib.CDC_E_DEVICE
+        monkeypatch.delenv("CDC_BACKUP_FAIL_DEVICE")
+        objs, packs, st = s.run(paths)
+    assert st["failed_files"] == 0
+    ref_objs = snapshot.chunkify_batch(files)
+    for o, r, b in zip(objs, ref_objs, files):
+        assert o.Checksum == r.Checksum == hashlib.sha256(b).digest()
+        assert [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks]
+
+
 def test_backup_stats_report_the_hardware_queues():
     """cdc_backup_new records GPU_MAX_HW_QUEUES (0: unset, HIP's default of 4)
     and whether the pipeline's streams share hardware queues."""

@@ -60,19 +60,6 @@ _MASKL_ENV = os.environ.get("CDC_MASKL_INDEX", "1")[:1]
 _MASKL_MODE = int(_MASKL_ENV) if _MASKL_ENV in ("0", "1", "2", "3") else 1
 
 
-# the suite's resolution mode (CDC_RESOLVE_MODE), restored after each test
-_RESOLVE_MODE = 1 if os.environ.get("CDC_RESOLVE_MODE", "0")[:1] == "1" else 0
-
-
-@pytest.fixture(params=[1, 0], ids=["one-launch", "two-launch"])
-def resolve(request):
-    """Both resolution paths: k_chunk (scan + resolution in one launch) and
-    k_scan + k_resolve."""
-    device.set_resolve_mode(request.param)
-    yield request.param
-    device.set_resolve_mode(_RESOLVE_MODE)
-
-
 @pytest.fixture(autouse=True)
 def _reset_debug():
     device.set_debug_mode(0)
@@ -89,7 +76,7 @@ def _golden_cases():
 
 
 @pytest.mark.parametrize("case", _golden_cases(), ids=lambda c: c["name"])
-def test_device_matches_golden(oracle, resolve, case):
+def test_device_matches_golden(oracle, case):
     import sys
     sys.path.insert(0, GOLDEN)
     import make_golden as mg
@@ -113,7 +100,7 @@ PARAMS = [
 @pytest.mark.parametrize("p", PARAMS, ids=lambda p: f"{p['min_size']}-{p['normal_size']}-{p['max_size']}")
 @pytest.mark.parametrize("kind", ["random", "low_entropy", "zeros", "mixed"])
 @pytest.mark.parametrize("cut_adj", [0, 1])
-def test_device_param_sweep(oracle, resolve, p, kind, cut_adj):
+def test_device_param_sweep(oracle, p, kind, cut_adj):
     n = 3 << 20
     if kind == "random":
         data = random_bytes(n, 21)
@@ -129,7 +116,7 @@ def test_device_param_sweep(oracle, resolve, p, kind, cut_adj):
 
 
 @pytest.mark.parametrize("size", [0, 1, 63, 64, 65, 1000, 65535, 65536, 65537, 65536 + 49, 1 << 20, (4 << 20) + 1, 9_999_999])
-def test_device_sizes(oracle, resolve, size):
+def test_device_sizes(oracle, size):
     data = random_bytes(size, size)
     gear = _placeholder()
     (got,), res = gpu_chunk([data], DEF, gear=gear)
@@ -139,7 +126,7 @@ def test_device_sizes(oracle, resolve, size):
 
 
 @pytest.mark.parametrize("off", [1, 3, 7, 8, 13, 15])
-def test_device_unaligned(oracle, resolve, off):
+def test_device_unaligned(oracle, off):
     p = dict(min_size=2048, normal_size=8192, max_size=65536)
     data = random_bytes((1 << 20) + off * 7, off)
     gear = gear_table(off)
@@ -147,7 +134,7 @@ def test_device_unaligned(oracle, resolve, off):
     assert_same(got, oracle.chunk(data, gear, **p), f"offset {off}")
 
 
-def test_device_dense_candidates(oracle, resolve):
+def test_device_dense_candidates(oracle):
     """G[0] = 0: every all-zero window hits MaskS, so every index block
     overflows and the chains never merge (offset-preserving): exercises the
     dense raw rescans and the sequential fallback resolver."""
@@ -158,7 +145,7 @@ def test_device_dense_candidates(oracle, resolve):
     assert_same(got, oracle.chunk(data, gear, **DEF), "dense")
 
 
-def test_device_alternative_masks(oracle, resolve):
+def test_device_alternative_masks(oracle):
     """Masks are runtime parameters (v0.0.8 values unverified)."""
     ms, ml = 0x0000000000001FFF, 0x00000000000001FF   # low bits: W = 13
     _lib.ensure_init(gear=gear_table(50), mask_s=ms, mask_l=ml)
@@ -242,7 +229,7 @@ def test_maskl_index_alternative_masks(oracle, masks, mode):
 
 # ---------------------------------------------------------------- debug resolver
 @pytest.mark.parametrize("kind", ["random", "low_entropy"])
-def test_sequential_resolver_matches(oracle, resolve, kind):
+def test_sequential_resolver_matches(oracle, kind):
     data = random_bytes(16 << 20, 60) if kind == "random" else low_entropy(16 << 20, 61)
     gear = _placeholder()
     device.set_debug_mode(1)
@@ -253,7 +240,7 @@ def test_sequential_resolver_matches(oracle, resolve, kind):
 
 # ---------------------------------------------------------------- streaming windows
 @pytest.mark.parametrize("window", [(4 << 20) + 4096, 9 << 20, 33 << 20])
-def test_nonfinal_windows_compose(oracle, resolve, window):
+def test_nonfinal_windows_compose(oracle, window):
     """final = 0 windows + resume at `consumed` == the whole stream (the
     Peek(MaxSize) carry of ext chunker.go)."""
     data = np.concatenate([random_bytes(40 << 20, 70), low_entropy(20 << 20, 71)])
@@ -274,7 +261,7 @@ def test_nonfinal_windows_compose(oracle, resolve, window):
 
 
 # ---------------------------------------------------------------- batched buffers
-def test_batch_many_buffers(oracle, resolve):
+def test_batch_many_buffers(oracle):
     """Independent buffers in one launch group (and more than one group)."""
     p = dict(min_size=2048, normal_size=8192, max_size=65536)
     sizes = [0, 5, 2047, 2048, 70000, 1 << 20, 3 << 20] * 6
@@ -285,7 +272,7 @@ def test_batch_many_buffers(oracle, resolve):
         assert_same(got[i], oracle.chunk(a, gear, **p), f"buffer {i} ({a.size} B)")
 
 
-def test_pipelined_streams(oracle, resolve):
+def test_pipelined_streams(oracle):
     """Two batches over the same buffers alternate over two streams (bench.py's
     pipelined steps): one batch's resolution kernels run beside the next
     batch's scan; every pass must still produce the oracle's cut lists."""
@@ -304,7 +291,7 @@ def test_pipelined_streams(oracle, resolve):
             assert_same(c.cpu().numpy().astype(np.uint64), r, f"stream {k} buffer {i}")
 
 
-def test_c2_shape_32x64MiB(oracle, resolve):
+def test_c2_shape_32x64MiB(oracle):
     """BASELINE configs[2], one GPU's share: 32 x 64 MiB random buffers."""
     arrays = [random_bytes(64 << 20, 100 + i) for i in range(32)]
     gear = _placeholder()
@@ -313,7 +300,7 @@ def test_c2_shape_32x64MiB(oracle, resolve):
         assert_same(got[i], oracle.chunk(a, gear, **DEF), f"buffer {i}")
 
 
-def test_c1_full_1GiB(oracle, resolve):
+def test_c1_full_1GiB(oracle):
     """BASELINE configs[1]: 1 GiB random, default params, bit-exact."""
     data = random_bytes(1 << 30, 1)
     gear = _placeholder()
