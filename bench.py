@@ -175,7 +175,17 @@ def stream_read_peak(torch, L, bufs, dev, local, reps=20):
                 note="measured after the roofline loop; frac_of_measured_peak = achieved / best_GBps")
 
 
-def digest_leg(torch, batch, bufs, reps, check):
+# The host's CPU share per GPU: OMP_NUM_THREADS where the launcher sets it
+# (16 on the one-GPU box), else 16.
+def _cpu_share():
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    return int(v) if v.isdigit() and int(v) > 0 else 16
+
+
+CPU_SHARE = _cpu_share()
+
+
+def digest_leg(torch, batch, bufs, reps, check, host_threads=16):
     """Per-chunk SHA-256 + byte histogram (processChunk, snapshot/backup.go:594-629)
     over the device cut lists of the pass: device-resident, events around the
     digest kernels.  Not part of `value`.  On rank 0 of a 1-GPU run the first
@@ -207,19 +217,20 @@ def digest_leg(torch, batch, bufs, reps, check):
              bound="one launch lasts as long as its longest chunk's SHA-256 chain: 64-B blocks x ~905 VALU of one "
                    "round wave per block")
     # the hybrid single pass (cdc_chunk_digests_hybrid): the longest chunks'
-    # SHA-256 on 16 host cores (the box's CPU share), the rest on the device
+    # SHA-256 on host_threads host cores (--hybrid-threads: default the box's
+    # CPU share per GPU), the rest on the device
     if len(bufs) <= 32:
-        hout, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res_rows, host_threads=16)
+        hout, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res_rows, host_threads=host_threads)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            hout, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res_rows, host_threads=16)
+            hout, hc, hb = hashing.chunk_digests_hybrid(bufs, cut_lists, res_rows, host_threads=host_threads)
         torch.cuda.synchronize()
         hms = (time.perf_counter() - t0) / reps * 1e3
         same = all(torch.equal(a[0][:c.shape[0]], b[0][:c.shape[0]]) and torch.equal(a[1][:c.shape[0]], b[1][:c.shape[0]])
                    for a, b, c in zip(out, hout, cuts))
         d["hybrid"] = dict(value=round(total / (hms * 1e-3) / GIB, 2), unit="GiB/s", ms_per_pass=round(hms, 3),
-                           host_threads=16, host_chunks=hc, host_bytes=hb, equal_to_device_only=bool(same),
+                           host_threads=host_threads, host_chunks=hc, host_bytes=hb, equal_to_device_only=bool(same),
                            note="cdc_chunk_digests_hybrid, wall time incl. the cut lists back to the host: the "
                                 "longest chunks' SHA-256 on host cores (x86 SHA extensions, ~35 ns per 64-B block "
                                 "against a device chain's ~2 us), the rest and every histogram on the device")
@@ -684,7 +695,12 @@ def main():
                     help="only the roofline loop (--steps single-stream passes after --warmup ones; no timed "
                          "pipelined region, no side legs): under rocprofv3 --kernel-trace --stats the k_scan "
                          "average of the summary is the line's roofline.kernel_avg_ms")
-    ap.add_argument("--backup-readers", type=int, default=16, help="c4b: reader threads (reads + object SHA-256)")
+    ap.add_argument("--backup-readers", type=int, default=CPU_SHARE,
+                    help="c4b: reader threads (reads + object SHA-256); default the CPU share per GPU")
+    ap.add_argument("--hybrid-threads", type=int, default=CPU_SHARE * 3 // 2,
+                    help="host threads of the hybrid per-chunk SHA-256 leg; default 1.5 x the CPU share per GPU "
+                         "(threads wait on the copy-back parts: 24 on 16 CPUs beat 16 by 10 %, 32 no better; "
+                         "profiles/r06_host_threads_ab.txt)")
     ap.add_argument("--backup-packers", type=int, default=8, help="c4b: packer threads")
     ap.add_argument("--backup-batch-mib", type=int, default=512,
                     help="c4b: bytes per device batch (MiB; 512 measured best of 256 / 512 / 1024, profiles/r04_c4b_batch.txt)")
@@ -915,7 +931,7 @@ def main():
 
     digest = None
     if not host_mode and args.digest_reps > 0:
-        digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0)
+        digest = digest_leg(torch, batch, bufs, args.digest_reps, rank == 0, args.hybrid_threads)
         digest["pipelined_with_chunking"] = chunk_digest_pipeline(torch, bufs, opts, dev, args.digest_window, 8)
 
     encode_res = None
