@@ -887,7 +887,13 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
 #endif
 }
 
-__global__ __launch_bounds__(kS2Waves * 64) void k_scan(const Batch B, const DevParams P, const Workspace W)
+// CDC_SCAN_LB (build-time A/B, with CDC_SCAN_WAVES=8): the launch bound the
+// scan is compiled for; 768 keeps an 8-wave scan at <= 168 VGPRs (the
+// 12-wave budget), leaving room on each SIMD for a k_resolve wave.
+#ifndef CDC_SCAN_LB
+#define CDC_SCAN_LB (kS2Waves * 64)
+#endif
+__global__ __launch_bounds__(CDC_SCAN_LB) void k_scan(const Batch B, const DevParams P, const Workspace W)
 {
     scan_body<false>(B, P, W);
 }
@@ -900,7 +906,7 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan_l(const Batch B, const D
 // Both indexes in one pass (launched instead of k_scan + k_scan_l while the
 // adaptive hint says the MaskL index is needed): the MaskL key is a window of
 // the same fingerprint, one v_alignbit + v_and and half a v_min3 per byte.
-__global__ __launch_bounds__(kS2Waves * 64) void k_scan_f(const Batch B, const DevParams P, const Workspace W)
+__global__ __launch_bounds__(CDC_SCAN_LB) void k_scan_f(const Batch B, const DevParams P, const Workspace W)
 {
     scan_body<false, true>(B, P, W);
 }
@@ -2189,7 +2195,15 @@ __device__ __forceinline__ void write_empty_rows(const Batch &B, uint32_t lane)
     }
 }
 
-__global__ __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B, const DevParams P, const Workspace W)
+// CDC_RESOLVE_WAVES_PER_EU (build-time A/B): cap k_resolve's registers (3:
+// <= 168 VGPRs) so that one of its waves fits on a SIMD beside the scan's
+// waves of the next pass.
+#ifdef CDC_RESOLVE_WAVES_PER_EU
+#define CDC_RESOLVE_ATTR __attribute__((amdgpu_waves_per_eu(CDC_RESOLVE_WAVES_PER_EU)))
+#else
+#define CDC_RESOLVE_ATTR
+#endif
+__global__ CDC_RESOLVE_ATTR __launch_bounds__(kWalkWavesPerWG * 64) void k_resolve(const Batch B, const DevParams P, const Workspace W)
 {
     __builtin_amdgcn_s_setprio(3);  // latency-bound: issue ahead of a co-resident scan (next batch)
     __shared__ uint64_t s_tab[256 * kWCopies];
