@@ -67,9 +67,13 @@ def buffer_seeds(wl, rank, world):
     return [1 + rank * wl["nbuf"] + i for i in range(wl["nbuf"])]
 
 
+def _dist_on(dist):
+    return dist is not None and dist.is_available() and dist.is_initialized()
+
+
 def reduce_max(dist, world, value, dev):
     """Max over ranks of a host float (the slowest rank sets the job time)."""
-    if world == 1:
+    if not _dist_on(dist):
         return value
     import torch
     t = torch.tensor([value], dtype=torch.float64,
@@ -489,7 +493,7 @@ def parity_check(bufs_host, cuts, opts, budget_bytes=1 << 30):
 
 def reduce_and(dist, world, flag, dev):
     """AND over ranks of a host bool (None counts as False)."""
-    if world == 1:
+    if not _dist_on(dist):
         return bool(flag)
     import torch
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -617,7 +621,7 @@ def spawn_ranks(argv, n):
 
 def gather_per_rank(dist, world, value, dev):
     """Every rank's host float, in rank order (rank 0 reports each rank's rate)."""
-    if world == 1:
+    if not _dist_on(dist):
         return [value]
     import torch
     on = dev if dist.get_backend() == "nccl" else "cpu"
@@ -767,7 +771,14 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # BENCH_DIST_ONE_RANK=1: a one-rank nccl (RCCL) process group even at
+    # N = 1, so the launch, barrier, max-over-ranks and gather code of the
+    # N-GPU run executes over RCCL on a one-GPU box (tests/test_gpu_scale.py)
+    one_rank_dist = world == 1 and os.environ.get("BENCH_DIST_ONE_RANK") == "1"
+    if one_rank_dist:
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+    if world > 1 or one_rank_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if rehearse:
             dist.init_process_group("gloo", rank=rank, world_size=world, timeout=dist_timeout())
@@ -775,7 +786,7 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=dist_timeout())
 
     def barrier():
-        if world > 1:
+        if _dist_on(dist):
             dist.barrier()
 
     wl = WORKLOADS[args.workload]
@@ -1000,6 +1011,7 @@ def main():
                   "chunk_params": "FASTCDC min 65536 / normal 1048576 / max 4194304",
                   "gear": "placeholder (v0.0.8 table unavailable; see DESIGN.md)",
                   "parallelism": f"independent buffers, 1 rank per GPU x {world}, no collective",
+                  "dist_backend": dist.get_backend() if _dist_on(dist) else None,
                   "per_rank_gibs": [round(per_rank_bytes * timed_steps / e / GIB, 2) if timed_steps else None
                                     for e in per_rank],
                   "chunks_per_step": nchunks,
@@ -1111,7 +1123,7 @@ def main():
         import shutil
         fbatch.close()
         shutil.rmtree(tmpdir, ignore_errors=True)
-    if world > 1:
+    if _dist_on(dist):
         dist.destroy_process_group()
     sys.stdout.flush()
     sys.stderr.flush()

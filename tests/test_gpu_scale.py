@@ -119,6 +119,26 @@ def test_bench_spawns_two_ranks_on_one_gpu():
     assert d["cpu_baseline"] is not None and d["cpu_baseline"]["value"] > 0, d
 
 
+def test_bench_rccl_path_one_rank():
+    """The N-GPU run's RCCL code -- init_process_group("nccl") with the
+    device id, the barriers around the timed region, the max-over-ranks
+    all_reduce, the per-rank all_gather and the parity AND, all on device
+    tensors -- executed on a one-GPU box by a one-rank process group
+    (BENCH_DIST_ONE_RANK=1).  Two ranks cannot share one GPU under RCCL, so
+    this is the closest the box gets to the 8-GPU run's collective path."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["BENCH_DIST_ONE_RANK"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
+           "--size-mib", "64", "--no-cpu-baseline", "--digest-reps", "0", "--encode-reps", "0", "--e2e-reps", "0"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["config"]["dist_backend"] == "nccl", d["config"]
+    assert d["n_gpus"] == 1 and len(d["config"]["per_rank_gibs"]) == 1 and d["value"] > 0, d
+    assert d["parity_vs_oracle"] is True, d
+
+
 def test_sequential_fallback_cost_1GiB(oracle):
     """The sequential fallback (debug mode 1 forces it) on a 1 GiB buffer: the
     cliff a buffer whose speculative chains never merge would hit.  Bit-exact,
