@@ -16,10 +16,9 @@ _URANDOM_SPLIT = 256 << 10  # above this, os.urandom in parallel pieces
 _urandom_pool = None
 
 
-def _urandom(n):
-    """os.urandom(n); a large draw (a batch of ~20 K blobs needs 1.2 MB, ~4 ms
-    from one thread) in four pieces on threads (getrandom releases the GIL):
-    the same kernel CSPRNG, ~2x sooner."""
+def _urandom_now(n):
+    """os.urandom(n); a large draw in four pieces on threads (getrandom
+    releases the GIL): the same kernel CSPRNG, ~2x sooner."""
     global _urandom_pool
     if n <= _URANDOM_SPLIT:
         return os.urandom(n)
@@ -29,6 +28,99 @@ def _urandom(n):
     k = 4
     sizes = [n // k + (1 if i < n % k else 0) for i in range(k)]
     return b"".join(_urandom_pool.map(os.urandom, sizes))
+
+
+class _Reservoir:
+    """OS random bytes drawn ahead of the calls that use them: a background
+    thread keeps up to `target` bytes of os.urandom output ready (in 256-KiB
+    pieces), and each Encode call takes fresh bytes from it (never the same
+    bytes twice), the rest drawn at once when the reservoir runs short.  The
+    source is the same kernel CSPRNG; only the time of the draw moves off the
+    call (a batch of ~20 K blobs needs 1.2 MB, 2-4.5 ms of getrandom).
+    DESIGN.md 5.7."""
+
+    PIECE = 256 << 10
+
+    def __init__(self, target=4 << 20):
+        import collections
+        import threading
+        self.target = target
+        self.pieces = collections.deque()  # bytes objects, consumed from the left
+        self.have = 0
+        self.mu = threading.Lock()
+        self.want = threading.Event()
+        self.thread = None
+
+    def _fill(self):
+        while True:
+            self.want.wait()
+            with self.mu:
+                if self.have >= self.target:
+                    self.want.clear()
+                    continue
+            piece = os.urandom(self.PIECE)
+            with self.mu:
+                self.pieces.append(piece)
+                self.have += len(piece)
+
+    def take_into(self, n):
+        """n fresh bytes in this thread's reusable buffer (no allocation once
+        it has grown: a fresh 1.2-MB bytes object costs ~1 ms of page faults);
+        returned as a ctypes char array over it, valid until this thread's
+        next call (cdc_encode_device copies the bytes before it returns)."""
+        import ctypes
+        import threading
+        tl = self.__dict__.setdefault("_tl", threading.local())
+        buf = getattr(tl, "buf", None)
+        if buf is None or len(buf) < n:
+            buf = tl.buf = bytearray(max(n, 1))
+        mv = memoryview(buf)
+        got = 0
+        with self.mu:
+            while got < n and self.pieces:
+                p = self.pieces.popleft()
+                k = min(len(p), n - got)
+                mv[got:got + k] = p[:k] if k < len(p) else p
+                if k < len(p):
+                    self.pieces.appendleft(p[k:])
+                got += k
+                self.have -= k
+            if self.thread is None:
+                self.thread = threading.Thread(target=self._fill, name="plakar-urandom-reservoir", daemon=True)
+                self.thread.start()
+        self.want.set()
+        if got < n:
+            mv[got:n] = _urandom_now(n - got)
+        mv.release()
+        return (ctypes.c_char * n).from_buffer(buf)
+
+    def take(self, n):
+        parts, got = [], 0
+        with self.mu:
+            while got < n and self.pieces:
+                p = self.pieces.popleft()
+                k = min(len(p), n - got)
+                parts.append(p[:k] if k < len(p) else p)
+                if k < len(p):
+                    self.pieces.appendleft(p[k:])
+                got += k
+                self.have -= k
+            if self.thread is None:
+                import threading
+                self.thread = threading.Thread(target=self._fill, name="plakar-urandom-reservoir", daemon=True)
+                self.thread.start()
+        self.want.set()
+        if got < n:
+            parts.append(_urandom_now(n - got))
+        return b"".join(parts)
+
+
+_reservoir = _Reservoir()
+
+
+def _urandom(n):
+    """n fresh OS random bytes for Encode's subkeys and nonces."""
+    return _reservoir.take(n)
 
 
 def encode_bound(n, compress=True, encrypt=True):
@@ -53,13 +145,15 @@ def encode_device(base, offsets, lens, out, key=None, compress=True, random=None
         key = bytes(key)
         if len(key) != 32:
             raise ValueError("the repository key is 32 bytes (AES-256)")
-        if random is None:
-            random = _urandom(RANDOM_BYTES * n)
-        if len(random) != RANDOM_BYTES * n:
+        if random is None:  # fresh OS random bytes, drawn ahead (the reservoir)
+            random = _reservoir.take_into(RANDOM_BYTES * n)
+        elif len(random) != RANDOM_BYTES * n:
             raise ValueError(f"random: {RANDOM_BYTES} bytes per blob")
+        else:
+            random = bytes(random)
     st = stream if stream is not None else torch.cuda.current_stream(device)
     check(lib().cdc_encode_device(int(device), ctypes.c_void_p(base.data_ptr()), offs, lns, n, int(bool(compress)),
-                                  key, bytes(random) if key is not None else None, ctypes.c_void_p(out.data_ptr()),
+                                  key, random if key is not None else None, ctypes.c_void_p(out.data_ptr()),
                                   out.numel(), oo, ctypes.c_void_p(st.cuda_stream)), "cdc_encode_device")
     return oo_a.astype(np.int64)
 
