@@ -50,6 +50,24 @@ class _Reservoir:
         self.mu = threading.Lock()
         self.want = threading.Event()
         self.thread = None
+        self.pid = os.getpid()
+        # a fork while the filler holds mu must not leave the child's lock held
+        os.register_at_fork(after_in_child=self._reset_lock)
+
+    def _reset_lock(self):
+        import threading
+        self.mu = threading.Lock()
+
+    def _after_fork(self):
+        """A forked child must never use bytes its parent may also use (GCM
+        nonce reuse): drop them and start its own filler.  Called under mu."""
+        import threading
+        if self.pid != os.getpid():
+            self.pieces.clear()
+            self.have = 0
+            self.thread = None
+            self.want = threading.Event()
+            self.pid = os.getpid()
 
     def _fill(self):
         while True:
@@ -60,6 +78,8 @@ class _Reservoir:
                     continue
             piece = os.urandom(self.PIECE)
             with self.mu:
+                if self.pid != os.getpid():
+                    return
                 self.pieces.append(piece)
                 self.have += len(piece)
 
@@ -77,6 +97,7 @@ class _Reservoir:
         mv = memoryview(buf)
         got = 0
         with self.mu:
+            self._after_fork()
             while got < n and self.pieces:
                 p = self.pieces.popleft()
                 k = min(len(p), n - got)
@@ -97,6 +118,7 @@ class _Reservoir:
     def take(self, n):
         parts, got = [], 0
         with self.mu:
+            self._after_fork()
             while got < n and self.pieces:
                 p = self.pieces.popleft()
                 k = min(len(p), n - got)
