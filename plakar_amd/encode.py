@@ -50,6 +50,7 @@ class _Reservoir:
         self.mu = threading.Lock()
         self.want = threading.Event()
         self.thread = None
+        self.tl = threading.local()  # each thread's reusable output buffer (take_into)
         self.pid = os.getpid()
         # a fork while the filler holds mu must not leave the child's lock held
         os.register_at_fork(after_in_child=self._reset_lock)
@@ -90,10 +91,9 @@ class _Reservoir:
         next call (cdc_encode_device copies the bytes before it returns)."""
         import ctypes
         import threading
-        tl = self.__dict__.setdefault("_tl", threading.local())
-        buf = getattr(tl, "buf", None)
+        buf = getattr(self.tl, "buf", None)
         if buf is None or len(buf) < n:
-            buf = tl.buf = bytearray(max(n, 1))
+            buf = self.tl.buf = bytearray(max(n, 1))
         mv = memoryview(buf)
         got = 0
         with self.mu:
