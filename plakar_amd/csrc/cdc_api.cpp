@@ -144,7 +144,7 @@ DevParams make_params(const cdc_opts *o)
     P.fs_lo = uint32_t(ms);
     P.fs_hi = uint32_t(ms >> 32);
     P.fl_sh = g.mask_l ? uint32_t(__builtin_clzll(g.mask_l)) : 0u;  // 63 - highest MaskL bit
-    P.fm_ws = P.fm_m = P.fm_ok = 0u;
+    P.fm_ws = P.fm_m = P.fm_ok = P.fm_mi = 0u;
     if (g.mask_l && __builtin_clzll(g.mask_l) >= int(P.fs_sh)) {  // MaskL << fs_sh keeps every bit
         const uint64_t lf = g.mask_l << P.fs_sh;
         const uint32_t hb = 63u - uint32_t(__builtin_clzll(lf)), lb = uint32_t(__builtin_ctzll(lf));
@@ -152,7 +152,10 @@ DevParams make_params(const cdc_opts *o)
         if (lb >= ws && ws <= 31u) {
             P.fm_ws = ws;
             P.fm_m = uint32_t(lf >> ws);
-            P.fm_ok = 1u;
+            P.fm_mi = uint32_t(ms >> ws) & P.fm_m;
+            // under 8 shared bits the filter fires on most groups: two
+            // passes (k_scan + k_scan_l) are cheaper then
+            P.fm_ok = __builtin_popcount(P.fm_mi) >= 8 ? 1u : 0u;
         }
     }
     const uint64_t ml = g.mask_l << P.fl_sh;

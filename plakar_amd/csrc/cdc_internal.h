@@ -52,8 +52,10 @@ struct DevParams {
     uint32_t fl_sh, fl_lo, fl_hi;
     // MaskL inside the MaskS frame (k_scan_f): the 32-bit window of fp' from
     // bit fm_ws holds every bit of MaskL << fs_sh; its mask fm_m.  fm_ok = 0
-    // when no such window exists (then k_scan + k_scan_l only).
-    uint32_t fm_ws, fm_m, fm_ok;
+    // when no such window exists (then k_scan + k_scan_l only).  fm_mi: the
+    // bits of MaskS and MaskL both, in that window -- k_scan_f's one filter
+    // key, necessary for a MaskS or a MaskL hit.
+    uint32_t fm_ws, fm_m, fm_ok, fm_mi;
 };
 
 struct BufDesc {

@@ -669,6 +669,7 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     const int32_t lag = int32_t(kStage * half);
     const uint32_t vhi = to_vgpr(kMaskL ? P.fl_hi : P.fs_hi);
     const uint32_t vlm = kFused ? to_vgpr(P.fm_m) : 0u, lws = P.fm_ws;  // k_scan_f: MaskL window
+    const uint32_t vim = kFused ? to_vgpr(P.fm_mi) : 0u;                  // k_scan_f: MaskS & MaskL there
     const uint32_t xlo = kMaskL ? P.fl_lo : P.fs_lo, xhi = kMaskL ? P.fl_hi : P.fs_hi;
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
     using C0 = std::integral_constant<uint32_t, 0>;
@@ -804,15 +805,16 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
                     const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
                     fp = (fp << 1) + cg[k];
                     ng[k] = lds_gear(tab, a0);
-                    const uint32_t k0 = uint32_t(fp >> 32) & vhi;
-                    uint32_t l0 = 0;
-                    if constexpr (kFused) l0 = __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm;
+                    // k_scan: the hi dword of MaskS; k_scan_f: the bits MaskS
+                    // and MaskL share (one key for both records)
+                    const uint32_t k0 = kFused ? __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vim
+                                               : uint32_t(fp >> 32) & vhi;
                     const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
                     fp = (fp << 1) + cg[k + 1];
                     ng[k + 1] = lds_gear(tab, a1);
-                    acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
-                    if constexpr (kFused)
-                        acc = umin3(acc, l0, __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vlm);
+                    acc = umin3(acc, k0,
+                                kFused ? __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vim
+                                       : uint32_t(fp >> 32) & vhi);
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 __builtin_amdgcn_sched_barrier(0);

@@ -203,9 +203,11 @@ def test_maskl_adaptive_follows_the_data(oracle):
 
 @pytest.mark.parametrize("masks", [
     (0x0000000000001FFF, 0x00000000000001FF),  # MaskL inside MaskS's span: fused window exists
+    (0x0000000000001FF7, 0x00000000000003FF),  # 9 shared bits, MaskL bit 3 outside MaskS: fused
+    (0x0000000000001FFF, 0x0000000000001C01),  # 4 shared bits: too weak a filter, two passes
     (0x0000000000001FFF, 0x00000000000301FF),  # MaskL's top bit above MaskS's: no fused window
     (0x0003590703530000, 0x0000800000000001),  # MaskL spans 48 bits: no 32-bit window
-], ids=["fusable", "maskl-above", "maskl-wide"])
+], ids=["fusable", "fusable-lonly", "shared-weak", "maskl-above", "maskl-wide"])
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_maskl_index_alternative_masks(oracle, masks, mode):
     """The fused pass's MaskL window is derived from the masks; where none
