@@ -144,18 +144,19 @@ DevParams make_params(const cdc_opts *o)
     P.fs_lo = uint32_t(ms);
     P.fs_hi = uint32_t(ms >> 32);
     P.fl_sh = g.mask_l ? uint32_t(__builtin_clzll(g.mask_l)) : 0u;  // 63 - highest MaskL bit
-    P.fm_ws = P.fm_m = P.fm_ok = P.fm_mi = 0u;
-    if (g.mask_l && __builtin_clzll(g.mask_l) >= int(P.fs_sh)) {  // MaskL << fs_sh keeps every bit
-        const uint64_t lf = g.mask_l << P.fs_sh;
-        const uint32_t hb = 63u - uint32_t(__builtin_clzll(lf)), lb = uint32_t(__builtin_ctzll(lf));
-        const uint32_t ws = hb >= 31u ? hb - 31u : 0u;
-        if (lb >= ws && ws <= 31u) {
-            P.fm_ws = ws;
-            P.fm_m = uint32_t(lf >> ws);
-            P.fm_mi = uint32_t(ms >> ws) & P.fm_m;
-            // under 8 shared bits the filter fires on most groups: two
-            // passes (k_scan + k_scan_l) are cheaper then
-            P.fm_ok = __builtin_popcount(P.fm_mi) >= 8 ? 1u : 0u;
+    P.fm_sh = P.fm_mi = P.fm_llo = P.fm_lhi = P.fm_ok = 0u;
+    const uint64_t mi = g.mask_s & g.mask_l;  // the bits both masks test
+    // under 8 shared bits the filter fires on most groups: two passes
+    // (k_scan + k_scan_l) are cheaper then
+    if (g.mask_l && __builtin_clzll(g.mask_l) >= int(P.fs_sh) && __builtin_popcountll(mi) >= 8) {
+        const uint32_t lb = uint32_t(__builtin_ctzll(mi)), hb = 63u - uint32_t(__builtin_clzll(mi));
+        if (hb - lb <= 31u) {
+            P.fm_sh = lb < 32u ? 32u - lb : 0u;  // the lowest shared bit to bit 32 (hb + fm_sh <= 63)
+            P.fm_mi = uint32_t((mi << P.fm_sh) >> 32);
+            const uint64_t lf = g.mask_l << P.fs_sh;  // keeps every bit (the clz test)
+            P.fm_llo = uint32_t(lf);
+            P.fm_lhi = uint32_t(lf >> 32);
+            P.fm_ok = 1u;
         }
     }
     const uint64_t ml = g.mask_l << P.fl_sh;

@@ -50,12 +50,14 @@ struct DevParams {
     uint32_t fs_sh, fs_lo, fs_hi;
     // The same frame for MaskL (k_scan_l, the MaskL candidate index).
     uint32_t fl_sh, fl_lo, fl_hi;
-    // MaskL inside the MaskS frame (k_scan_f): the 32-bit window of fp' from
-    // bit fm_ws holds every bit of MaskL << fs_sh; its mask fm_m.  fm_ok = 0
-    // when no such window exists (then k_scan + k_scan_l only).  fm_mi: the
-    // bits of MaskS and MaskL both, in that window -- k_scan_f's one filter
-    // key, necessary for a MaskS or a MaskL hit.
-    uint32_t fm_ws, fm_m, fm_ok, fm_mi;
+    // k_scan_f (both indexes in one pass): its loop rolls fp << fm_sh, the
+    // frame whose hi dword holds every bit MaskS and MaskL share, and filters
+    // on those bits (fm_mi: a necessary key for a MaskS or a MaskL hit); its
+    // recheck rolls the MaskS frame, where MaskL << fs_sh = fm_lhi:fm_llo.
+    // fm_ok = 0 (then k_scan + k_scan_l only) when MaskL has a bit above
+    // MaskS's highest, or the shared bits are fewer than 8 or span more than
+    // 32.
+    uint32_t fm_sh, fm_mi, fm_llo, fm_lhi, fm_ok;
 };
 
 struct BufDesc {

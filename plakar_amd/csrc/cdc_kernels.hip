@@ -318,7 +318,9 @@ constexpr uint32_t kGearLdsBytes = 256u * 32u * 8u;   // 64 KiB
 // -2 % warm, profiles/r06_*).
 constexpr uint32_t kQCap = 64;
 constexpr uint32_t kQBytes = kQCap * 12u;
-static_assert(kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes) + 37128u <= 160u * 1024u,
+// k_scan_f's recheck table: the Gear table in the MaskS frame, one copy (2 KiB)
+constexpr uint32_t kFlushTabBytes = 256u * 8u;
+static_assert(kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes) + kFlushTabBytes + 37128u <= 160u * 1024u,
               "LDS budget: a scan workgroup and a k_resolve workgroup per CU");
 // Scan lane lengths are multiples of kLaneQuant (16-B aligned runs: every lane
 // of a buffer has the same stage alignment; 256 B avoided the slow strides
@@ -500,8 +502,9 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
 template <bool kMaskL, bool kFused = false>
 __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, const Workspace &W)
 {
-    static_assert(!(kMaskL && kFused), "k_scan_f builds both indexes in the MaskS frame");
-    __shared__ __attribute__((aligned(16))) char s_lds[kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes)];
+    static_assert(!(kMaskL && kFused), "k_scan_f builds both indexes, from the MaskS records' side");
+    __shared__ __attribute__((aligned(16)))
+    char s_lds[kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes) + (kFused ? kFlushTabBytes : 0u)];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t laneoff = (lane & 31u) << 3;
@@ -540,7 +543,14 @@ __device__ __forceinline__ void scan_body(const Batch &B, const DevParams &P, co
         g_ts[clk] = __builtin_amdgcn_s_memrealtime();
         g_ts[clk + 1] = __builtin_amdgcn_s_memtime();
     }
-    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear, kMaskL ? P.fl_sh : P.fs_sh);
+    fill_gear_lds<kS2Waves * 64>(reinterpret_cast<uint64_t *>(s_lds), W.gear,
+                                 kFused ? P.fm_sh : kMaskL ? P.fl_sh : P.fs_sh);
+    if constexpr (kFused) {  // the recheck's table: MaskS frame, one copy
+        static_assert(kS2Waves * 64 >= 256, "one entry per thread");
+        if (threadIdx.x < 256)
+            reinterpret_cast<uint64_t *>(s_lds + kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes))[threadIdx.x] =
+                W.gear[threadIdx.x] << P.fs_sh;
+    }
     __syncthreads();
     if (!kMaskL && threadIdx.x == 0) {
         dbg_ts(B, kTsScan + 4 * blockIdx.x + 1);
@@ -667,9 +677,9 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     };
     const uint32_t TT = T + 1;  // half 1 runs one stage behind
     const int32_t lag = int32_t(kStage * half);
-    const uint32_t vhi = to_vgpr(kMaskL ? P.fl_hi : P.fs_hi);
-    const uint32_t vlm = kFused ? to_vgpr(P.fm_m) : 0u, lws = P.fm_ws;  // k_scan_f: MaskL window
-    const uint32_t vim = kFused ? to_vgpr(P.fm_mi) : 0u;                  // k_scan_f: MaskS & MaskL there
+    // the loop's key: the hi dword of the frame (k_scan_f: the bits MaskS and
+    // MaskL share, in the frame fm_sh)
+    const uint32_t vhi = to_vgpr(kFused ? P.fm_mi : kMaskL ? P.fl_hi : P.fs_hi);
     const uint32_t xlo = kMaskL ? P.fl_lo : P.fs_lo, xhi = kMaskL ? P.fl_hi : P.fs_hi;
     const int64_t rel0 = int64_t(((ub + uint64_t(s)) & ~15ull) - kLead) - int64_t(ub);
     using C0 = std::integral_constant<uint32_t, 0>;
@@ -721,6 +731,16 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     uint32_t *const qm = reinterpret_cast<uint32_t *>(qf + kQCap);
     static_assert(kQCap == 64, "one flush pass: item j in lane j");
     uint32_t qn = 0;  // queued items (wave-uniform)
+    // The recheck's Gear entry for byte k of a 16-byte block: k_scan's own
+    // table; k_scan_f's one-copy MaskS-frame table (entry b at 8 b, after the
+    // queues) -- its loop's table is in another frame.
+    const char *const ftab = s_lds + kGearLdsBytes + kS2Waves * (kStageBytes + kQBytes);
+    auto rgear = [&](const uint4 &d, int k) -> uint64_t {
+        if constexpr (kFused)
+            return lds_gear(ftab, __builtin_amdgcn_ubfe(word_of(d, k >> 2), uint32_t(k & 3) * 8u, 8u) << 3);
+        else
+            return lds_gear(tab, gear_addr(laneoff, word_of(d, k >> 2), k));
+    };
     auto flush = [&]() {
         {
             const bool v = lane < qn;
@@ -730,16 +750,29 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
             const int64_t so = int64_t((seg0 + owner) * sl);  // the owner's run [so, so + ln)
             const int32_t ln = so < int64_t(D.len) ? int32_t(min(int64_t(sl), int64_t(D.len) - so)) : 0;
             const uint64_t a = ub + uint64_t(so + r0);  // 16-B aligned
-            const uint64_t a0 = min(max(a, lo_ok), hi_ok - 16u), a1 = min(max(a + 16u, lo_ok), hi_ok - 16u);
-            const uint4 d0 = gload16(a0), d1 = gload16(a1);
-            uint64_t f = qf[v ? lane : 0u];
+            auto clamp16 = [&](uint64_t x) { return min(max(x, lo_ok), hi_ok - 16u); };
+            const uint4 d0 = gload16(clamp16(a)), d1 = gload16(clamp16(a + 16u));
+            uint64_t f = 0;
+            if constexpr (kFused) {
+                // the loop's frame lacks MaskS's top bits: the fingerprint
+                // before the group is rolled again, in the MaskS frame, from
+                // the 64 bytes before it (bits < W depend on the last W bytes
+                // only; before the buffer's start, clamped bytes feed
+                // positions no walker reads)
+                uint4 dw[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) dw[h] = gload16(clamp16(a - 64u + 16u * uint32_t(h)));
+#pragma unroll
+                for (int k = 0; k < 64; ++k) f = (f << 1) + rgear(dw[k >> 4], k & 15);
+            } else {
+                f = qf[v ? lane : 0u];
+            }
             uint32_t miss = 0, missL = 0;
 #pragma unroll
             for (int k = 0; k < 32; ++k) {
-                f = (f << 1) + lds_gear(tab, gear_addr(laneoff, word_of(k < 16 ? d0 : d1, (k & 15) >> 2), k));
+                f = (f << 1) + rgear(k < 16 ? d0 : d1, k & 15);
                 miss |= min(key_of(f, xlo, xhi), 1u) << k;
-                if constexpr (kFused)
-                    missL |= min(__builtin_amdgcn_alignbit(uint32_t(f >> 32), uint32_t(f), lws) & vlm, 1u) << k;
+                if constexpr (kFused) missL |= min(key_of(f, P.fm_llo, P.fm_lhi), 1u) << k;
             }
             const int32_t lo = r0 < 0 ? -r0 : 0, hi = ln - r0;  // valid positions [0, ln) of the run
             uint32_t vm = lo >= 32 ? 0u : (0xFFFFFFFFu << lo);
@@ -805,16 +838,11 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
                     const uint32_t a0 = gear_addr(laneoff, word_of(nx, k >> 2), k);
                     fp = (fp << 1) + cg[k];
                     ng[k] = lds_gear(tab, a0);
-                    // k_scan: the hi dword of MaskS; k_scan_f: the bits MaskS
-                    // and MaskL share (one key for both records)
-                    const uint32_t k0 = kFused ? __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vim
-                                               : uint32_t(fp >> 32) & vhi;
+                    const uint32_t k0 = uint32_t(fp >> 32) & vhi;
                     const uint32_t a1 = gear_addr(laneoff, word_of(nx, (k + 1) >> 2), k + 1);
                     fp = (fp << 1) + cg[k + 1];
                     ng[k + 1] = lds_gear(tab, a1);
-                    acc = umin3(acc, k0,
-                                kFused ? __builtin_amdgcn_alignbit(uint32_t(fp >> 32), uint32_t(fp), lws) & vim
-                                       : uint32_t(fp >> 32) & vhi);
+                    acc = umin3(acc, k0, uint32_t(fp >> 32) & vhi);
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -837,7 +865,7 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
                         const uint32_t idx =
                             qn + __builtin_amdgcn_mbcnt_hi(uint32_t(fm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(fm), 0u));
                         const int32_t r0 = rr0 + int32_t(kStage * t + 16u * (gi - 1));
-                        qf[idx] = f0;
+                        if constexpr (!kFused) qf[idx] = f0;  // k_scan_f rolls it again
                         qm[idx] = uint32_t(r0 + 256) | (lane << 24);
                     }
                     qn += nq;
@@ -906,8 +934,9 @@ __global__ __launch_bounds__(kS2Waves * 64) void k_scan_l(const Batch B, const D
 }
 
 // Both indexes in one pass (launched instead of k_scan + k_scan_l while the
-// adaptive hint says the MaskL index is needed): the MaskL key is a window of
-// the same fingerprint, one v_alignbit + v_and and half a v_min3 per byte.
+// adaptive hint says the MaskL index is needed): the loop filters on the bits
+// MaskS and MaskL share, in a frame whose hi dword holds them (one v_and and
+// half a v_min3 per byte, as k_scan); the recheck tests both masks exactly.
 __global__ __launch_bounds__(CDC_SCAN_LB) void k_scan_f(const Batch B, const DevParams P, const Workspace W)
 {
     scan_body<false, true>(B, P, W);

@@ -202,17 +202,19 @@ def test_maskl_adaptive_follows_the_data(oracle):
 
 
 @pytest.mark.parametrize("masks", [
-    (0x0000000000001FFF, 0x00000000000001FF),  # MaskL inside MaskS's span: fused window exists
+    (0x0000000000001FFF, 0x00000000000001FF),  # MaskL inside MaskS's span: fused (loop frame 32)
     (0x0000000000001FF7, 0x00000000000003FF),  # 9 shared bits, MaskL bit 3 outside MaskS: fused
     (0x0000000000001FFF, 0x0000000000001C01),  # 4 shared bits: too weak a filter, two passes
-    (0x0000000000001FFF, 0x00000000000301FF),  # MaskL's top bit above MaskS's: no fused window
-    (0x0003590703530000, 0x0000800000000001),  # MaskL spans 48 bits: no 32-bit window
-], ids=["fusable", "fusable-lonly", "shared-weak", "maskl-above", "maskl-wide"])
+    (0x0000000000001FFF, 0x00000000000301FF),  # MaskL's top bit above MaskS's: two passes
+    (0x0003590703530000, 0x0000800000000001),  # MaskL spans 48 bits, no shared bit: two passes
+    (0x0003590703530000, 0x0000D90003530000),  # the FastCDC masks (10 shared bits, loop frame 16)
+], ids=["fusable", "fusable-lonly", "shared-weak", "maskl-above", "maskl-wide", "fastcdc"])
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_maskl_index_alternative_masks(oracle, masks, mode):
-    """The fused pass's MaskL window is derived from the masks; where none
-    exists, mode 2 falls back to k_scan + k_scan_l. At these sizes many
-    chunks pass Normal and end on MaskL candidates."""
+    """k_scan_f's loop frame and key are derived from the masks; where the
+    masks do not allow one (MaskL above MaskS, fewer than 8 shared bits), mode
+    2 falls back to k_scan + k_scan_l. At these sizes many chunks pass Normal
+    and end on MaskL candidates."""
     ms, ml = masks
     gear = gear_table(52)
     _lib.ensure_init(gear=gear, mask_s=ms, mask_l=ml)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 6: k_scan_f with one filter key (the bits MaskS and MaskL share)
-# against two keys (var_f2.so): the parity subset on the in-tree library, C3
+# against variants (var_*.so): the parity subset on each library, C3
 # lines interleaved twice, and the k_scan_f instruction counts
 # (CDC_MASKL_INDEX=2: the fused pass every launch group).
 #   tools/r06_c3ab.sh <tag> variant.so ...
@@ -9,8 +9,12 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_abort.py -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_base.log" 2>&1 || { tail -20 "$OUT/pytest_base.log"; exit 1; }
-echo "base: $(tail -1 $OUT/pytest_base.log)"
+for v in base "$@"; do
+  lib=""; [ "$v" != base ] && lib="$PWD/plakar_amd/_lib/$v"
+  n=${v%.so}
+  PLAKAR_CDC_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_abort.py -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_$n.log" 2>&1 || { tail -20 "$OUT/pytest_$n.log"; exit 1; }
+  echo "$n: $(tail -1 $OUT/pytest_$n.log)"
+done
 QUIET="--no-cpu-baseline --e2e-reps 0 --digest-reps 0 --encode-reps 0"
 for rep in 1 2; do
   for v in base "$@"; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 evidence on the final code: GPU suite, smoke, the driver's exact bench command (three times, plain) and
 # under a rocprofv3 kernel trace (+ per-pass timeline), the roofline loop alone under a trace, bench lines
-# C1-C4 / c4f / c4b (twice) / c4bl, the N = 2 rank rehearsal and the one-rank RCCL run on one GPU, PMC passes of
+# C1-C4 (C3 also under a kernel trace) / c4f / c4b (twice) / c4bl, the N = 2 rank rehearsal and the one-rank RCCL run on one GPU, PMC passes of
 # the C1 scan (FETCH_SIZE; instruction counts) and of the C3 fused scan (instruction counts).
 #   tools/r06_final.sh <tag> [skip-suite]
 TAG=${1:-r06final}
@@ -41,6 +41,12 @@ for wl in c2 c3; do
     timeout -k 10 300 python3 bench.py --workload $wl --no-cpu-baseline > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.err" || exit 1
     cut -c1-200 "$OUT/bench_$wl.json"
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c3_ktrace" -o run -- \
+    python3 bench.py --workload c3 --steps 50 --warmup 50 --no-cpu-baseline --e2e-reps 0 --digest-reps 0 --encode-reps 0 \
+    > "$OUT/c3_ktrace_bench.json" 2> "$OUT/c3_ktrace.err" || exit 1
+f=$(ls $OUT/c3_ktrace/*/run_kernel_trace.csv $OUT/c3_ktrace/run_kernel_trace.csv 2>/dev/null | head -1)
+python tools/kstats.py "$f" > "$OUT/c3_kernel_summary.txt"
+head -6 "$OUT/c3_kernel_summary.txt"
 timeout -k 10 400 python3 bench.py --workload c4 --steps 3 --warmup 1 --cpu-seconds 10 > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err" || exit 1
 timeout -k 10 400 python3 bench.py --workload c4f --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/bench_c4f.json" 2> "$OUT/bench_c4f.err" || exit 1
 timeout -k 10 500 python3 bench.py --workload c4b --steps 5 --warmup 2 > "$OUT/bench_c4b.json" 2> "$OUT/bench_c4b.err" || exit 1
