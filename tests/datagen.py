@@ -34,3 +34,28 @@ def zipf_sizes(count, seed, s=1.1, unit=4096, kmax=32768):
 def gear_table(seed):
     """Alternative Gear tables for parity tests (the real v0.0.8 table is unknown)."""
     return [int(x) for x in np.random.PCG64(seed).random_raw(256)]
+
+
+def _bits_mask(rng, bits, top):
+    """`bits` distinct random bits below `top`."""
+    return int(sum(1 << int(b) for b in rng.choice(top, size=bits, replace=False)))
+
+
+def draw_masks(rng, default):
+    """Random (MaskS, MaskL) for the randomised parity tests: `default` (the
+    FastCDC pair), MaskL drawn from MaskS's bits (nested), mostly shared bits
+    plus one of MaskL's own, or independent masks."""
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        return default
+    top = int(rng.integers(20, 64))
+    ms = _bits_mask(rng, int(rng.integers(9, 16)), top)
+    bits = [b for b in range(64) if ms >> b & 1]
+    if kind == 1:
+        ml = int(sum(1 << int(b) for b in rng.choice(bits, size=max(1, len(bits) - 3), replace=False)))
+    elif kind == 2:
+        ml = int(sum(1 << int(b) for b in rng.choice(bits, size=max(1, len(bits) - 4), replace=False)))
+        ml |= 1 << int(rng.integers(0, top))
+    else:
+        ml = _bits_mask(rng, int(rng.integers(6, 13)), int(rng.integers(16, 64)))
+    return ms, ml

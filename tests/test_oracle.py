@@ -6,8 +6,8 @@ import os
 import numpy as np
 import pytest
 
-from datagen import gear_table, low_entropy, random_bytes
-from oracle_ref import py_algorithm, py_chunk
+from datagen import draw_masks, gear_table, low_entropy, random_bytes
+from oracle_ref import DEFAULT_MASK_L, DEFAULT_MASK_S, py_algorithm, py_chunk
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -113,3 +113,23 @@ def test_validate_bounds(oracle):
     assert oracle.validate(1 << 20, 1 << 20, 4 << 20) == -2
     assert oracle.validate(65536, 1 << 20, 1 << 20) == -3
     assert oracle.validate(65536, 1 << 20, (1 << 30) + 1) == -3
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_oracle_random_masks_match_python(oracle, seed):
+    """Random masks (the ones tests/test_gpu_fuzz.py draws: nested, mostly
+    shared, independent) and parameters: the C oracle and the pure-Python
+    restatement agree, so the GPU fuzz cases are checked against a restatement
+    that is itself cross-checked."""
+    rng = np.random.default_rng(np.random.PCG64(9000 + seed))
+    ms, ml = draw_masks(rng, (DEFAULT_MASK_S, DEFAULT_MASK_L))
+    mn = 64 << int(rng.integers(0, 4))
+    p = dict(min_size=mn, normal_size=mn << int(rng.integers(1, 4)), max_size=0)
+    p["max_size"] = p["normal_size"] << int(rng.integers(1, 3))
+    data = np.concatenate([random_bytes(12000, seed), low_entropy(12000, seed + 1, 0.02),
+                           np.zeros(4000, np.uint8)])
+    gear = gear_table(9100 + seed)
+    cut_adj = int(rng.integers(0, 2))
+    c = oracle.chunk(data, gear, mask_s=ms, mask_l=ml, cut_adj=cut_adj, **p)
+    ref = py_chunk(data.tobytes(), gear, mask_s=ms, mask_l=ml, cut_adj=cut_adj, **p)
+    assert [tuple(map(int, r)) for r in c] == ref, f"masks {ms:#x}/{ml:#x} {p}"
