@@ -720,8 +720,9 @@ __device__ __forceinline__ void scan_task(const Batch &B, const DevParams &P, co
     const int32_t rr0 = int32_t(rel0 - s) - lag;
     // The recheck queue.  A lane whose filter fired in a 32-byte group queues
     // that group -- fp before it, its offset in the run and the lane: 12 bytes
-    // of LDS -- and the wave rechecks the queue, one item per lane, at the end
-    // of the task or when the queue is full.
+    // of LDS (k_scan_f: the offset and lane only, 4 bytes) -- and the wave
+    // rechecks the queue, one item per lane, at the end of the task or when
+    // the queue is full.
     // The group's bytes are read again from memory then (aligned 16-byte
     // loads, clamped into the buffer; bytes outside the run only feed
     // positions the valid mask drops), so nothing of the group has to stay in
