@@ -11,7 +11,9 @@ from plakar_amd import encode
 def _fresh():
     r = encode._Reservoir(target=1 << 20)
     r.take(1)  # starts the filler
-    time.sleep(0.3)
+    t0 = time.monotonic()
+    while r.have < r.target and time.monotonic() - t0 < 10:  # a loaded host may be slow to fill
+        time.sleep(0.05)
     return r
 
 
