@@ -1607,44 +1607,22 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     if (st != CDC_OK) return st;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool encrypt = key != nullptr;
-    // plan on the host: blobs, 4-MiB blocks, 16-KiB segments, frame slots
-    std::vector<BlobDesc> blobs(n);
-    std::vector<Blk> blks;
-    std::vector<Seg> segs;
+    // plan on the host: blobs, 4-MiB blocks, 8-KiB segments, frame slots.
+    // Counted first, then written straight into the pinned staging at their
+    // workspace offsets (no vectors, no copy).
+    size_t nk = 0, ng = 0;
     uint64_t slot = 0, pieces_max = 0;
     for (uint32_t b = 0; b < n; ++b) {
-        BlobDesc &D = blobs[b];
-        D.src = offsets[b];
-        D.len = lens[b];
-        D.blk0 = uint32_t(blks.size());
-        D.nblk = compress ? uint32_t((lens[b] + kBlockLZ - 1) / kBlockLZ) : 0u;
-        for (uint32_t k = 0; k < D.nblk; ++k) {
-            Blk K{};
-            K.src = offsets[b] + k * kBlockLZ;
-            K.len = uint32_t(std::min<uint64_t>(kBlockLZ, lens[b] - k * kBlockLZ));
-            K.blob = b;
-            K.k = k;
-            K.seg0 = uint32_t(segs.size());
-            K.nseg = (K.len + kSegLZ - 1) / kSegLZ;
-            for (uint32_t g = 0; g < K.nseg; ++g) {
-                Seg S{};
-                S.src = K.src + uint64_t(g) * kSegLZ;
-                S.len = std::min<uint32_t>(kSegLZ, K.len - g * kSegLZ);
-                S.rem = K.len - g * kSegLZ;
-                segs.push_back(S);
-            }
-            blks.push_back(K);
-        }
-        const uint64_t fmax = compress ? 7 + 4ull * D.nblk + lens[b] + 8 : lens[b];
-        D.slot = slot;
+        const uint64_t nblk = compress ? (lens[b] + kBlockLZ - 1) / kBlockLZ : 0;
+        nk += nblk;
+        if (nblk) ng += (nblk - 1) * ((kBlockLZ + kSegLZ - 1) / kSegLZ) +
+                        (lens[b] - (nblk - 1) * kBlockLZ + kSegLZ - 1) / kSegLZ;
+        const uint64_t fmax = compress ? 7 + 4ull * nblk + lens[b] + 8 : lens[b];
         slot += align16(fmax);
         pieces_max += encrypt ? (fmax + kPiece - 1) / kPiece : 0;
     }
-    std::vector<uint32_t> xx_ids(n);  // XXH32 order: longest first (a wave's blobs end together)
-    for (uint32_t b = 0; b < n; ++b) xx_ids[b] = b;
-    std::stable_sort(xx_ids.begin(), xx_ids.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
     // one device allocation for the plan and the workspace
-    const size_t nb = blobs.size(), nk = blks.size(), ng = segs.size();
+    const size_t nb = n;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -1673,6 +1651,70 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
                    hipEventCreateWithFlags(&C.fork, hipEventDisableTiming) != hipSuccess ||
                    hipEventCreateWithFlags(&C.join, hipEventDisableTiming) != hipSuccess))
         return CDC_E_DEVICE;
+    // The plan's tables at their workspace offsets [0, o_key + 32) in pinned
+    // staging, XXH32 order after them: two DMAs.  (The call ends with a
+    // stream sync under C.mu, so the staging is free again on return.)
+    const size_t h_prefix = o_key + 32, h_xx = align16(h_prefix), h_need = h_xx + (compress ? nb * 4 : 0);
+    if (C.hcap < h_need) {
+        if (C.hp) (void)hipHostFree(C.hp);
+        C.hp = nullptr;
+        C.hcap = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&C.hp), h_need, hipHostMallocDefault) != hipSuccess)
+            return CDC_E_NOMEM;
+        C.hcap = h_need;
+    }
+    {
+        BlobDesc *blobs = reinterpret_cast<BlobDesc *>(C.hp + o_blobs);
+        Blk *blks = reinterpret_cast<Blk *>(C.hp + o_blks);
+        Seg *segs = reinterpret_cast<Seg *>(C.hp + o_segs);
+        uint32_t kb = 0, kg = 0;
+        uint64_t sl = 0;
+        for (uint32_t b = 0; b < n; ++b) {
+            BlobDesc D{};
+            D.src = offsets[b];
+            D.len = lens[b];
+            D.blk0 = kb;
+            D.nblk = compress ? uint32_t((lens[b] + kBlockLZ - 1) / kBlockLZ) : 0u;
+            for (uint32_t k = 0; k < D.nblk; ++k) {
+                Blk K{};
+                K.src = offsets[b] + k * kBlockLZ;
+                K.len = uint32_t(std::min<uint64_t>(kBlockLZ, lens[b] - k * kBlockLZ));
+                K.blob = b;
+                K.k = k;
+                K.seg0 = kg;
+                K.nseg = (K.len + kSegLZ - 1) / kSegLZ;
+                for (uint32_t g = 0; g < K.nseg; ++g) {
+                    Seg S{};
+                    S.src = K.src + uint64_t(g) * kSegLZ;
+                    S.len = std::min<uint32_t>(kSegLZ, K.len - g * kSegLZ);
+                    S.rem = K.len - g * kSegLZ;
+                    segs[kg++] = S;
+                }
+                blks[kb++] = K;
+            }
+            const uint64_t fmax = compress ? 7 + 4ull * D.nblk + lens[b] + 8 : lens[b];
+            D.slot = sl;
+            sl += align16(fmax);
+            blobs[b] = D;
+        }
+        if (kb != nk || kg != ng) return CDC_E_INVALID;  // the counting pass and the plan disagree (a bug)
+        if (encrypt) {
+            std::memcpy(C.hp + o_rnd, random, nb * 56);
+            std::memcpy(C.hp + o_key, key, 32);
+        }
+        if (compress && nb) {
+            // XXH32 order: longest first (a wave's blobs end together); ties by
+            // index, so the order is the stable one.  Keys (~len, index) sort
+            // without an indirection per comparison.
+            thread_local std::vector<uint64_t> xk;
+            xk.resize(nb);
+            for (uint32_t b = 0; b < n; ++b)
+                xk[b] = (uint64_t(0xFFFFFFFFu - uint32_t(std::min<uint64_t>(lens[b], 0xFFFFFFFFu))) << 32) | b;
+            std::sort(xk.begin(), xk.end());
+            uint32_t *xx = reinterpret_cast<uint32_t *>(C.hp + h_xx);
+            for (size_t i = 0; i < nb; ++i) xx[i] = uint32_t(xk[i]);
+        }
+    }
     Batch Bt{};
     Bt.base = static_cast<const uint8_t *>(d_base);
     Bt.nblobs = n;
@@ -1703,34 +1745,9 @@ extern "C" int cdc_encode_device(int device, const void *d_base, const uint64_t 
     Bt.status = reinterpret_cast<uint64_t *>(ws + o_status);
     Bt.xx_ids = reinterpret_cast<uint32_t *>(ws + o_xx);
     const uint32_t xx_wgs = (n + kXxWaves * kXxPerWave - 1) / (kXxWaves * kXxPerWave);
-    bool ok = true;
-    // The plan's tables at their workspace offsets [0, o_key + 32) in pinned
-    // staging, XXH32 order after them: two DMAs.  (The call ends with a
-    // stream sync under C.mu, so the staging is free again on return.)
-    const size_t h_prefix = o_key + 32, h_xx = align16(h_prefix), h_need = h_xx + (compress ? nb * 4 : 0);
-    if (C.hcap < h_need) {
-        if (C.hp) (void)hipHostFree(C.hp);
-        C.hp = nullptr;
-        C.hcap = 0;
-        if (hipHostMalloc(reinterpret_cast<void **>(&C.hp), h_need, hipHostMallocDefault) != hipSuccess)
-            return CDC_E_NOMEM;
-        C.hcap = h_need;
-    }
-    auto stage = [&](size_t o, const void *p, size_t bytes) {
-        if (bytes) std::memcpy(C.hp + o, p, bytes);
-    };
-    stage(o_blobs, blobs.data(), nb * sizeof(BlobDesc));
-    stage(o_blks, blks.data(), nk * sizeof(Blk));
-    stage(o_segs, segs.data(), ng * sizeof(Seg));
-    if (encrypt) {
-        stage(o_rnd, random, nb * 56);
-        stage(o_key, key, 32);
-    }
-    ok = hipMemcpyAsync(ws, C.hp, h_prefix, hipMemcpyHostToDevice, s) == hipSuccess;
-    if (compress && nb) {
-        stage(h_xx, xx_ids.data(), nb * 4);
+    bool ok = hipMemcpyAsync(ws, C.hp, h_prefix, hipMemcpyHostToDevice, s) == hipSuccess;
+    if (compress && nb)
         ok = ok && hipMemcpyAsync(ws + o_xx, C.hp + h_xx, nb * 4, hipMemcpyHostToDevice, s) == hipSuccess;
-    }
     if (ok && n) {
         if (compress) {
             ok = hipEventRecord(C.fork, s) == hipSuccess && hipStreamWaitEvent(C.aux, C.fork, 0) == hipSuccess;
