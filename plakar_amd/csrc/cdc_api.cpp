@@ -16,6 +16,7 @@
 #include <cstring>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1107,6 +1108,67 @@ HybridScratch &hybrid_scratch(int device)
     return h[device & 63];
 }
 
+// Host threads for the hybrid digests' SHA-256, kept between calls (one pool
+// per device, used under that device's HybridScratch lock): starting 23
+// threads per call cost about a millisecond.  The threads are detached and
+// live for the process; a forked child cannot use the device, so it never
+// runs a job.
+struct HostPool {
+    std::mutex mu;
+    std::condition_variable go, done;
+    const std::function<void()> *job = nullptr;
+    uint64_t gen = 0;
+    int nthreads = 0, want = 0, busy = 0;
+
+    // f on n - 1 pool threads and the caller; returns when every one is done
+    void run(int n, const std::function<void()> &f)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            try {
+                while (nthreads < n - 1) {
+                    std::thread([this, id = nthreads] { loop(id); }).detach();
+                    ++nthreads;
+                }
+            } catch (...) {  // fewer threads: the work is shared by the ones there are
+            }
+            job = &f;
+            want = std::min(n - 1, nthreads);
+            busy = want;
+            ++gen;
+        }
+        go.notify_all();
+        f();
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return busy == 0; });
+        job = nullptr;
+    }
+
+    void loop(int id)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void()> *j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                go.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+                if (id >= want) continue;  // not counted for this job
+                j = job;
+            }
+            (*j)();
+            std::lock_guard<std::mutex> lk(mu);
+            if (--busy == 0) done.notify_all();
+        }
+    }
+};
+
+HostPool &host_pool(int device)
+{
+    static HostPool *p = new HostPool[64];  // never destroyed: its threads outlive static destruction
+    return p[device & 63];
+}
+
 bool hy_dev(void *&p, uint64_t &cap, uint64_t need)
 {
     if (need <= cap && p) return true;
@@ -1240,9 +1302,17 @@ int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64
             L[q] = c.offset >= lens[i] ? 0ull : std::min<uint64_t>(c.length, lens[i] - c.offset);
             bof[q] = i;
         }
+    // longest first, ties in row order: one sort of (~length, row) keys
+    // (lengths are clipped chunk lengths, < 2^32)
     std::vector<uint64_t> order(total);
-    for (uint64_t q = 0; q < total; ++q) order[q] = q;
-    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return L[a] > L[b]; });
+    if (total < (1ull << 32)) {
+        for (uint64_t q = 0; q < total; ++q) order[q] = (uint64_t(0xFFFFFFFFu - uint32_t(std::min<uint64_t>(L[q], 0xFFFFFFFFu))) << 32) | q;
+        std::sort(order.begin(), order.end());
+        for (uint64_t q = 0; q < total; ++q) order[q] &= 0xFFFFFFFFull;
+    } else {
+        for (uint64_t q = 0; q < total; ++q) order[q] = q;
+        std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return L[a] > L[b]; });
+    }
     size_t k = 0;
     if (host_min_len) {
         while (k < total && L[order[k]] >= host_min_len) ++k;
@@ -1359,14 +1429,10 @@ int cdc_chunk_digests_hybrid(int device, const void *const *d_data, const uint64
             sha256(hstage + soff[j], size_t(L[order[j]]), hdig + 32 * j);
         }
     };
-    std::vector<std::thread> ts;
-    try {
-        for (int t = 1; t < host_threads; ++t) ts.emplace_back(worker);
-    } catch (...) {
-        fail.store(CDC_E_NOMEM);
+    {
+        const std::function<void()> job = worker;
+        host_pool(device).run(host_threads, job);
     }
-    worker();
-    for (auto &t : ts) t.join();
     if (fail.load() != CDC_OK) return fail.load();
     // the host's digests into their rows, after the device's digest kernel
     if (hipStreamWaitEvent(H.side, H.ev_dig, 0) != hipSuccess ||
