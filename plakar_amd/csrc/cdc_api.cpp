@@ -1119,12 +1119,17 @@ struct HostPool {
     const std::function<void()> *job = nullptr;
     uint64_t gen = 0;
     int nthreads = 0, want = 0, busy = 0;
+    pid_t pid = 0;  // the process the threads belong to (a forked child has none of them)
 
     // f on n - 1 pool threads and the caller; returns when every one is done
     void run(int n, const std::function<void()> &f)
     {
         {
             std::lock_guard<std::mutex> lk(mu);
+            if (pid != getpid()) {
+                pid = getpid();
+                nthreads = 0;
+            }
             try {
                 while (nthreads < n - 1) {
                     std::thread([this, id = nthreads] { loop(id); }).detach();
