@@ -42,7 +42,7 @@ WORKLOADS = {
                     "share), host buffers in -> cut lists in host memory (PCIe-inclusive)",
                nbuf=512, size=0, kind="zipf", host=True),
     "c4f": dict(desc="C4 from files: the same 512-file share written to disk once (untimed), then per step read by the "
-                     "library (pread, 16 threads) into its pinned arena and chunked (pinned H2D, cut lists to host), "
+                     "library (pread, --file-threads: half the CPU share) into its pinned arena and chunked (pinned H2D, cut lists to host), "
                      "the reads running ahead of the device by 256-MiB sub-batches; warm page cache",
                 nbuf=512, size=0, kind="zipf", host=True, files=True),
     "c4b": dict(desc="C4 end-to-end backup: the same 512-file share written to disk once (untimed), then per step "
@@ -705,6 +705,9 @@ def main():
                     help="host threads of the hybrid per-chunk SHA-256 leg; default 1.5 x the CPU share per GPU "
                          "(threads wait on the copy-back parts: 24 on 16 CPUs beat 16 by 10 %, 32 no better; "
                          "profiles/r06_host_threads_ab.txt)")
+    ap.add_argument("--file-threads", type=int, default=max(1, CPU_SHARE // 2),
+                    help="c4f: pread threads filling the pinned arena; default half the CPU share per GPU "
+                         "(4-8 threads read 37-41 GiB/s on 16 CPUs, 16 threads 33-37: profiles/r06_c4f_threads_ab.txt)")
     ap.add_argument("--backup-packers", type=int, default=8, help="c4b: packer threads")
     ap.add_argument("--backup-batch-mib", type=int, default=512,
                     help="c4b: bytes per device batch (MiB; 512 measured best of 256 / 512 / 1024, profiles/r04_c4b_batch.txt)")
@@ -831,7 +834,7 @@ def main():
 
             def step():
                 fbatch.reset()
-                return fbatch.add_and_chunk(paths, opts, threads=16)
+                return fbatch.add_and_chunk(paths, opts, threads=args.file_threads)
 
             if wl.get("backup"):
                 from plakar_amd import snapshot
