@@ -20,7 +20,10 @@ from plakar_amd import _lib, chunkers, device  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 128
+import os  # noqa: E402
+
+N_CASES = int(os.environ.get("FUZZ_CASES", "128"))  # a longer sweep: FUZZ_CASES=2000
+N_STREAM = int(os.environ.get("FUZZ_STREAM_CASES", "32"))
 
 
 @pytest.fixture(autouse=True)
@@ -106,7 +109,7 @@ def test_random_configuration(oracle, seed):
             assert int(res[i, 1]) == a.size, f"{what}: buffer {i} consumed {int(res[i, 1])}"
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", range(N_STREAM))
 def test_random_stream_windows(oracle, seed):
     """A stream chunked as non-final windows (each resumed at the last
     window's `consumed`, the Peek(MaxSize) carry of the Go chunker's Next)
