@@ -144,3 +144,32 @@ def test_random_stream_windows(oracle, seed):
     assert got.shape == ref.shape, f"{what}: {got.shape[0]} chunks vs {ref.shape[0]}"
     bad = np.nonzero((got != ref).any(axis=1))[0]
     assert bad.size == 0, f"{what}: chunk {bad[0]}: {got[bad[0]]} vs {ref[bad[0]]}"
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_host_buffers(oracle, seed, monkeypatch):
+    """cdc_chunk (host buffers in, cut lists out, through the two-slot staging
+    pipeline) on random configurations: 1-40 buffers, launch-group budgets of
+    16 MiB-1 GiB, and buffers above CDC_HOST_MAXBUF_MB chunked as streams of
+    windows."""
+    rng = np.random.default_rng(np.random.PCG64(8000 + seed))
+    gear = _lib.default_gear() if rng.random() < 0.3 else gear_table(8100 + seed)
+    ms, ml = _masks(rng)
+    p = _params(rng)
+    cut_adj = int(rng.integers(0, 2))
+    monkeypatch.setenv("CDC_HOST_GROUP_MB", str(int(rng.choice([16, 64, 1024]))))
+    monkeypatch.setenv("CDC_HOST_MAXBUF_MB", str(int(rng.choice([16, 64, 16384]))))
+    device.set_maskl_index_mode(int(rng.integers(0, 4)))
+    nb = int(rng.integers(1, 41))
+    sizes = [_size(rng) if rng.random() < 0.9 else int(rng.integers(16 << 20, 40 << 20)) for _ in range(nb)]
+    datas = [_data(rng, n, 8200 + 64 * seed + i) for i, n in enumerate(sizes)]
+    _lib.ensure_init(gear=gear, mask_s=ms, mask_l=ml, cut_convention=cut_adj)
+    res = chunkers.ChunkBuffers(datas, chunkers.ChunkerOpts(MinSize=p["min_size"], NormalSize=p["normal_size"],
+                                                             MaxSize=p["max_size"]))
+    what = f"seed {seed}: masks {ms:#x}/{ml:#x} {p} cut_adj {cut_adj} sizes {sizes}"
+    for i, a in enumerate(datas):
+        ref = oracle.chunk(a, gear, mask_s=ms, mask_l=ml, cut_adj=cut_adj, **p)
+        got = np.asarray(res[i]).astype(np.uint64).reshape(-1, 2)
+        assert got.shape == ref.shape, f"{what}: buffer {i}: {got.shape[0]} chunks vs {ref.shape[0]}"
+        bad = np.nonzero((got != ref).any(axis=1))[0]
+        assert bad.size == 0, f"{what}: buffer {i}: chunk {bad[0]}: {got[bad[0]]} vs {ref[bad[0]]}"
