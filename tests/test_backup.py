@@ -315,3 +315,60 @@ def test_backup_many_small_files_rotate_every_slot(tmp_path):
         assert sum(c.Length for c in o.Chunks) == len(b), i
     want = {c.Checksum for o in objs for c in o.Chunks}
     assert set(_blobs_of(packs, KEY, True)) == want and st["new_blobs"] == len(want)
+
+
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("BACKUP_FUZZ_CASES", "8"))))
+def test_backup_random_corpora(tmp_path, seed):
+    """Random corpora through the whole pipeline: 1-40 files of 0 B-24 MiB
+    (duplicates and shared prefixes among them), random chunking sizes, batch
+    sizes that cut large files into pieces, reader / packer counts, packfile
+    sizes and encodings.  Objects equal the batch path's (chunkify_batch: cut
+    points vs the oracle, digests vs hashlib); every stored blob decodes to its
+    chunk's bytes, once."""
+    from plakar_amd.chunking import Configuration
+    from plakar_amd.repository import Repository
+    rng = np.random.default_rng(np.random.PCG64(9500 + seed))
+    mn = 4096 << int(rng.integers(0, 5))
+    cfg = Configuration("FASTCDC", mn, mn << int(rng.integers(1, 4)), 0)
+    cfg.MaxSize = cfg.NormalSize << int(rng.integers(1, 3))
+    repo = Repository(cfg)
+    files = []
+    for i in range(int(rng.integers(1, 41))):
+        r = rng.random()
+        if files and r < 0.1:
+            files.append(files[int(rng.integers(0, len(files)))])  # a duplicate
+        elif files and r < 0.2:
+            f = files[int(rng.integers(0, len(files)))]
+            files.append(f[:len(f) // 2] + random_bytes(int(rng.integers(1, 1 << 20)), 9600 + 64 * seed + i).tobytes())
+        else:
+            n = 0 if r < 0.25 else int(np.exp(rng.uniform(0, np.log(24 << 20))))
+            gen = random_bytes if rng.random() < 0.7 else (lambda k, s: low_entropy(k, s, 0.01))
+            files.append(gen(n, 9700 + 64 * seed + i).tobytes())
+    paths = []
+    for i, b in enumerate(files):
+        p = tmp_path / f"f{i:02d}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    key, compression = [(KEY, "LZ4"), (None, None), (None, "LZ4"), (KEY, None)][seed % 4]
+    batch = int(rng.choice([4 << 20, 8 << 20, 32 << 20]))
+    objs, packs, st = snapshot.backup_files(paths, repo=repo, key=key, compression=compression,
+                                            max_size=int(rng.choice([1 << 20, 4 << 20, 20 << 20])),
+                                            packers=int(rng.integers(1, 5)), readers=int(rng.integers(1, 9)),
+                                            batch_bytes=batch, timestamp=seed)
+    what = f"seed {seed}: {cfg} batch {batch} sizes {[len(f) for f in files]}"
+    ref_objs = snapshot.chunkify_batch(files, repo=repo)
+    assert len(objs) == len(files), what
+    want = {}
+    for i, (o, r) in enumerate(zip(objs, ref_objs)):
+        assert o.Checksum == r.Checksum == hashlib.sha256(files[i]).digest(), f"{what}: file {i}"
+        assert [c.Length for c in o.Chunks] == [c.Length for c in r.Chunks], f"{what}: file {i}"
+        assert [c.Checksum for c in o.Chunks] == [c.Checksum for c in r.Chunks], f"{what}: file {i}"
+        off = 0
+        for c in o.Chunks:
+            want[c.Checksum] = files[i][off:off + c.Length]
+            off += c.Length
+    blobs = _blobs_of(packs, key, compression == "LZ4")
+    assert set(blobs) == set(want), what
+    for c, plain in blobs.items():
+        assert plain == want[c], what
+    assert st["bytes"] == sum(len(f) for f in files) and st["new_blobs"] == len(want), what
