@@ -242,3 +242,33 @@ def test_encode_device_offsets_across_tensors():
     host = out.cpu().numpy()
     for i, s in enumerate(src):
         assert ref.decode(host[oo[i]:oo[i + 1]].tobytes(), key=KEY) == s
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_encode_random_batches(seed):
+    """Random batches: 1-300 blobs of 0 B-9 MiB (across the 64-KiB GCM pieces,
+    the 8-KiB match segments and the 4-MiB LZ4 blocks), random, low-entropy,
+    repetitive and text-like contents, each encoding; every blob comes back
+    through DecryptStream + the LZ4 frame reader."""
+    rng = np.random.default_rng(np.random.PCG64(4200 + seed))
+    blobs = []
+    for i in range(int(rng.integers(1, 301))):
+        r = rng.random()
+        n = 0 if r < 0.05 else int(rng.choice([65536, 4 << 20, 8192])) + int(rng.integers(-2, 3)) if r < 0.2 \
+            else int(np.exp(rng.uniform(0, np.log(9 << 20))))
+        n = max(0, n)
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            b = random_bytes(n, 4300 + 512 * seed + i).tobytes()
+        elif k == 1:
+            b = low_entropy(n, 4300 + 512 * seed + i, 0.02).tobytes()
+        elif k == 2:
+            b = (random_bytes(int(rng.integers(1, 300)), i).tobytes() * (n // 7 + 1))[:n]
+        else:
+            b = (b"backup snapshot chunk packfile plakar %d " % i * (n // 30 + 1))[:n]
+        blobs.append(b)
+    key = KEY if seed % 3 != 2 else None
+    compress = seed % 2 == 0
+    outs = encode.encode_blobs(blobs, key=key, compress=compress)
+    for i, (b, o) in enumerate(zip(blobs, outs)):
+        assert ref.decode(o, key=key, compressed=compress) == b, f"seed {seed} blob {i} ({len(b)} B)"
