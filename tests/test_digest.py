@@ -432,3 +432,39 @@ def test_gpu_chunkify_batch_objects(oracle):
             tot += n
         assert o.Entropy == (tot_e / float(tot) if tot else 0.0)
         assert list(o.Distribution) == [0.0] * 256
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_digest_random_cut_lists(seed):
+    """Random buffers and cut lists (chunks of 0 B-600 KiB at any alignment,
+    gaps and overlaps allowed, result rows that bound the counts) through the
+    device-only batch path and the hybrid path at a random split and thread
+    count: every digest equals hashlib, every histogram numpy.bincount."""
+    torch = _gpu()
+    from plakar_amd import _lib, hashing
+    _lib.ensure_init()
+    rng = np.random.default_rng(np.random.PCG64(7700 + seed))
+    bufs, cut_lists, res, refs = [], [], [], []
+    for k in range(int(rng.integers(1, 9))):
+        data = random_bytes(int(rng.integers(1, 6 << 20)), 7800 + 16 * seed + k)
+        cuts = []
+        for _ in range(int(rng.integers(0, 200))):
+            o = int(rng.integers(0, data.size))
+            n = int(min(data.size - o, np.exp(rng.uniform(0, np.log(600 << 10))) if rng.random() > 0.05 else 0))
+            cuts.append((o, n))
+        keep = len(cuts) if rng.random() < 0.7 else int(rng.integers(0, len(cuts) + 1))
+        bufs.append(torch.from_numpy(data).cuda())
+        cut_lists.append(torch.tensor(np.asarray(cuts or [(0, 0)], np.int64).reshape(-1, 2), device="cuda"))
+        res.append(torch.tensor([keep if cuts else 0, 0, 0, 0], dtype=torch.int64, device="cuda"))
+        refs.append((data, cuts[:keep]))
+    outs = hashing.chunk_digests_batch(bufs, cut_lists, res)
+    torch.cuda.synchronize()
+    for (data, cuts), (d, h) in zip(refs, outs):
+        _check(data, cuts, d[:len(cuts)].cpu().numpy(), h[:len(cuts)].cpu().numpy())
+    host_min_len = int(rng.choice([0, 1, 100_000]))
+    outs, _, _ = hashing.chunk_digests_hybrid(bufs, cut_lists, res, host_threads=int(rng.integers(1, 25)),
+                                              host_min_len=host_min_len)
+    torch.cuda.synchronize()
+    for (data, cuts), (d, h) in zip(refs, outs):
+        _check(data, cuts, d[:len(cuts)].cpu().numpy(), h[:len(cuts)].cpu().numpy())
