@@ -173,3 +173,51 @@ def test_random_host_buffers(oracle, seed, monkeypatch):
         assert got.shape == ref.shape, f"{what}: buffer {i}: {got.shape[0]} chunks vs {ref.shape[0]}"
         bad = np.nonzero((got != ref).any(axis=1))[0]
         assert bad.size == 0, f"{what}: buffer {i}: chunk {bad[0]}: {got[bad[0]]} vs {ref[bad[0]]}"
+
+
+class _RaggedReader:
+    """An io.Reader that returns 1..k bytes per read (no readinto)."""
+
+    def __init__(self, data, rng):
+        self.b = data.tobytes()
+        self.o = 0
+        self.rng = rng
+
+    def read(self, n):
+        k = min(n, int(self.rng.integers(1, 1 << int(self.rng.integers(1, 22)))))
+        out = self.b[self.o:self.o + k]
+        self.o += len(out)
+        return out
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_streaming_next(oracle, seed):
+    """NewChunker(...).Next() over a ragged reader (1 B - 2 MiB per read),
+    random configurations and window sizes: the chunks are the oracle's, byte
+    for byte, then (nil, EOF)."""
+    rng = np.random.default_rng(np.random.PCG64(6600 + seed))
+    gear = _lib.default_gear() if rng.random() < 0.3 else gear_table(6700 + seed)
+    ms, ml = _masks(rng)
+    p = _params(rng)
+    cut_adj = int(rng.integers(0, 2))
+    device.set_maskl_index_mode(int(rng.integers(0, 4)))
+    data = _data(rng, int(rng.integers(0, 12 << 20)), 6800 + seed)
+    window = int(rng.choice([0, 1, 3 << 20, 2 * p["max_size"] + 4096 + int(rng.integers(0, 1 << 20))]))
+    _lib.ensure_init(gear=gear, mask_s=ms, mask_l=ml, cut_convention=cut_adj)
+    ref = oracle.chunk(data, gear, mask_s=ms, mask_l=ml, cut_adj=cut_adj, **p)
+    opts = chunkers.ChunkerOpts(MinSize=p["min_size"], NormalSize=p["normal_size"], MaxSize=p["max_size"])
+    chk = chunkers.NewChunker("fastcdc", _RaggedReader(data, rng), opts, window_bytes=window)
+    what = f"seed {seed}: masks {ms:#x}/{ml:#x} {p} cut_adj {cut_adj} size {data.size} window {window}"
+    off, k = 0, 0
+    while True:
+        chunk, err = chk.Next()
+        if err is chunkers.EOF:
+            assert chunk is None, what
+            break
+        assert k < ref.shape[0], f"{what}: more chunks than the oracle's {ref.shape[0]}"
+        assert (int(ref[k, 0]), int(ref[k, 1])) == (off, len(chunk)), f"{what}: chunk {k}"
+        assert chunk == data[off:off + len(chunk)].tobytes(), f"{what}: chunk {k} bytes"
+        off += len(chunk)
+        k += 1
+    assert k == ref.shape[0] and off == data.size, what
+    chk.close()
