@@ -1111,8 +1111,8 @@ HybridScratch &hybrid_scratch(int device)
 // Host threads for the hybrid digests' SHA-256, kept between calls (one pool
 // per device, used under that device's HybridScratch lock): starting 23
 // threads per call cost about a millisecond.  The threads are detached and
-// live for the process; a forked child cannot use the device, so it never
-// runs a job.
+// live for the process (a forked child, which has none of them, starts its
+// own).
 struct HostPool {
     std::mutex mu;
     std::condition_variable go, done;
